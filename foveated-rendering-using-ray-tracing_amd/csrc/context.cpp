@@ -1,0 +1,756 @@
+// context.cpp — fr_ctx: device memory, stage orchestration and the C ABI of include/fovrt.h.
+//
+// Host-side counterpart of PathTracer (FR/PathTracer.cpp) and of the GL pass classes
+// (FR/JumpFlooding.cpp, FR/SibsonInterpolation.cpp, FR/PullPushInterpolation.cpp, FR/ATrous.cpp):
+// one HIP stream per context, every buffer allocated once in fr_create, zero host copies between
+// stages (the reference's PBO->texture copies, FR/PathTracer.cpp:253-305, disappear).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../include/fovrt.h"
+#include "fr_device.h"
+#include "scene.h"
+
+namespace fr {
+void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, DevStats*, hipStream_t);
+void launch_shade(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
+                  const f4*, f4*, f4*, DevStats*, hipStream_t);
+void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
+void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
+                     const f4*, f4*, uint8_t*, unsigned long long*, int, hipStream_t);
+void launch_mask_words(const uint8_t*, int, int, unsigned long long*, hipStream_t);
+void launch_compaction(int, int, const unsigned long long*, uint32_t*, uint32_t*, uint32_t*, hipStream_t);
+void launch_jfa(const f4*, uint32_t*, uint32_t*, f4*, f4*, int, int, hipStream_t);
+void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
+void launch_pullpush(const f4*, f4*, f4*, f4*, f4*, int, int, hipStream_t);
+void launch_atrous(const f4*, const f4*, const f4*, f4*, int, int, float, float, float, float, hipStream_t);
+int pp_size(int W, int H);
+size_t pp_snap_count(int S);
+}  // namespace fr
+
+using namespace fr;
+
+static thread_local std::string g_create_error;
+
+enum Phys {
+  P_POSITION, P_NORMAL, P_DEPTH_A, P_DEPTH_B, P_DIFFUSE, P_WEIGHT, P_HIST_A, P_HIST_B, P_SHADING, P_EXTRA,
+  P_JFA_COORD, P_JFA_COLOR, P_SIBSON, P_PULLPUSH, P_ATROUS_A, P_ATROUS_B, P_COUNT
+};
+
+struct fr_ctx {
+  fr_config cfg;
+  std::string asset_dir;
+  std::string err;
+  int W = 0, H = 0;
+  hipStream_t stream = nullptr;
+  HostScene scene;
+  Bvh bvh;
+  // device scene
+  BvhNode* d_nodes = nullptr;
+  TriGeo* d_tri = nullptr;
+  int32_t* d_prim = nullptr;
+  TriShade* d_shade = nullptr;
+  std::vector<f4*> d_tex;
+  DevMaterial* d_mats = nullptr;
+  DevTexture* d_texs = nullptr;
+  DevScene dsc;
+  // image buffers
+  f4* img[P_COUNT] = {};
+  int depth_cur = P_DEPTH_A, depth_cache = P_DEPTH_B;
+  int hist_cur = P_HIST_A, hist_cache = P_HIST_B;
+  int atrous_out = P_ATROUS_A;
+  uint8_t* mask = nullptr;
+  unsigned long long* words = nullptr;
+  uint32_t* offsets = nullptr;
+  uint32_t* ray_count = nullptr;
+  uint32_t* active = nullptr;
+  uint32_t *jfa_a = nullptr, *jfa_b = nullptr;
+  f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
+  int pp_S = 0;
+  DevStats* stats = nullptr;
+  FrameUniforms U;
+  uint32_t accum = 0;
+  bool light_pending = false;
+  bool compacted = false;
+  bool mask_dirty = false;
+  hipEvent_t ev[10] = {};
+  // scene export copies
+  std::vector<const float*> tex_ptrs;
+  std::vector<int32_t> tex_dims, mat_pairs;
+};
+
+namespace {
+
+int fail(fr_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg; else g_create_error = msg;
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                                 \
+  do {                                                                                                     \
+    hipError_t e_ = (expr);                                                                                \
+    if (e_ != hipSuccess) return fail(ctx, FR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+hipError_t dalloc(T** p, size_t count) {
+  hipError_t e = hipMalloc((void**)p, count * sizeof(T) + 16);
+  if (e != hipSuccess) return e;
+  return hipMemset(*p, 0, count * sizeof(T) + 16);
+}
+
+int check_launch(fr_ctx* c) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(c, FR_E_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+  return FR_OK;
+}
+
+// ---- glm-compatible camera math (FR/Camera.cpp; glm 0.9.x, GLM_FORCE_RADIANS) --------------
+struct Q { float w, x, y, z; };
+f3 qrot(Q q, f3 v) {  // glm::operator*(quat, vec3)
+  f3 qv = mk3(q.x, q.y, q.z);
+  f3 uv = cross(qv, v);
+  f3 uuv = cross(qv, uv);
+  return v + ((uv * q.w) + uuv) * 2.0f;
+}
+Q quat_cast(const float m[3][3]) {  // glm::quat_cast(mat3), m[col][row]
+  float fx = m[0][0] - m[1][1] - m[2][2];
+  float fy = m[1][1] - m[0][0] - m[2][2];
+  float fz = m[2][2] - m[0][0] - m[1][1];
+  float fw = m[0][0] + m[1][1] + m[2][2];
+  int bi = 0;
+  float fb = fw;
+  if (fx > fb) { fb = fx; bi = 1; }
+  if (fy > fb) { fb = fy; bi = 2; }
+  if (fz > fb) { fb = fz; bi = 3; }
+  float bv = sqrtf(fb + 1.0f) * 0.5f;
+  float mult = 0.25f / bv;
+  switch (bi) {
+    case 0: return Q{bv, (m[1][2] - m[2][1]) * mult, (m[2][0] - m[0][2]) * mult, (m[0][1] - m[1][0]) * mult};
+    case 1: return Q{(m[1][2] - m[2][1]) * mult, bv, (m[0][1] + m[1][0]) * mult, (m[2][0] + m[0][2]) * mult};
+    case 2: return Q{(m[2][0] - m[0][2]) * mult, (m[0][1] + m[1][0]) * mult, bv, (m[1][2] + m[2][1]) * mult};
+    default: return Q{(m[0][1] - m[1][0]) * mult, (m[2][0] + m[0][2]) * mult, (m[1][2] + m[2][1]) * mult, bv};
+  }
+}
+Q qnormalize(Q q) {
+  float len = sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+  if (len <= 0.0f) return Q{1, 0, 0, 0};
+  float inv = 1.0f / len;
+  return Q{q.w * inv, q.x * inv, q.y * inv, q.z * inv};
+}
+// column-major glm mat4 helpers: M[c][r]
+struct M4 { float m[4][4]; };
+M4 glm_lookat(f3 eye, f3 center, f3 up) {
+  f3 f = normalize(center - eye);
+  f3 s = normalize(cross(f, up));
+  f3 u = cross(s, f);
+  M4 r = {};
+  r.m[0][0] = s.x; r.m[1][0] = s.y; r.m[2][0] = s.z;
+  r.m[0][1] = u.x; r.m[1][1] = u.y; r.m[2][1] = u.z;
+  r.m[0][2] = -f.x; r.m[1][2] = -f.y; r.m[2][2] = -f.z;
+  r.m[3][0] = -dot(s, eye); r.m[3][1] = -dot(u, eye); r.m[3][2] = dot(f, eye);
+  r.m[3][3] = 1.0f;
+  return r;
+}
+M4 glm_perspective(float fovy, float aspect, float zn, float zf) {
+  float t = tanf(fovy / 2.0f);
+  M4 r = {};
+  r.m[0][0] = 1.0f / (aspect * t);
+  r.m[1][1] = 1.0f / t;
+  r.m[2][2] = -(zf + zn) / (zf - zn);
+  r.m[2][3] = -1.0f;
+  r.m[3][2] = -(2.0f * zf * zn) / (zf - zn);
+  return r;
+}
+M4 glm_mul(const M4& a, const M4& b) {  // glm mat4 * mat4
+  M4 r;
+  for (int c = 0; c < 4; c++)
+    for (int k = 0; k < 4; k++)
+      r.m[c][k] = a.m[0][k] * b.m[c][0] + a.m[1][k] * b.m[c][1] + a.m[2][k] * b.m[c][2] + a.m[3][k] * b.m[c][3];
+  return r;
+}
+void pose_matrices(const fr_camera_pose* p, M4& V, M4& P) {
+  Q q{p->rot[0], p->rot[1], p->rot[2], p->rot[3]};
+  f3 pos = mk3(p->pos[0], p->pos[1], p->pos[2]);
+  f3 front = qrot(q, mk3(0, 0, -1));
+  f3 upv = qrot(q, mk3(0, 1, 0));
+  V = glm_lookat(pos, pos + front, upv);
+  P = glm_perspective(p->fovy_deg * 0.01745329251994329576923690768489f, p->aspect, p->znear, p->zfar);
+}
+void to_rowmajor(const M4& a, float out[16]) {
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) out[r * 4 + c] = a.m[c][r];
+}
+bool invert_rowmajor(const float in[16], float out[16]) {  // Gauss-Jordan in f64, rounded once
+  double a[4][8];
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 8; c++) a[r][c] = c < 4 ? in[r * 4 + c] : (c - 4 == r ? 1.0 : 0.0);
+  for (int c = 0; c < 4; c++) {
+    int piv = c;
+    for (int r = c + 1; r < 4; r++) if (fabs(a[r][c]) > fabs(a[piv][c])) piv = r;
+    if (a[piv][c] == 0.0) return false;
+    if (piv != c) for (int k = 0; k < 8; k++) std::swap(a[c][k], a[piv][k]);
+    double d = a[c][c];
+    for (int k = 0; k < 8; k++) a[c][k] /= d;
+    for (int r = 0; r < 4; r++) {
+      if (r == c) continue;
+      double f = a[r][c];
+      for (int k = 0; k < 8; k++) a[r][k] -= f * a[c][k];
+    }
+  }
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) out[r * 4 + c] = (float)a[r][c + 4];
+  return true;
+}
+
+float elapsed(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.0f;
+  hipEventElapsedTime(&ms, a, b);
+  return ms;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+
+const char* fr_version(void) { return "fovrt 0.1 (gfx950)"; }
+
+int fr_config_default(fr_config* c) {
+  if (!c) return FR_E_INVALID;
+  memset(c, 0, sizeof(*c));
+  c->width = 1024; c->height = 1024;
+  c->scene = FR_SCENE_BUNNY;
+  c->mask_mode = FR_MASK_SALIENCY;
+  c->spp = 1;
+  c->diffuse_max_depth = 1;
+  c->refraction_max_depth = 16;
+  c->light_power = 810.0f;
+  c->optimize = 1;
+  c->atrous_iterations = 1;
+  c->write_extra = 1;
+  c->device = 0;
+  c->texture_mode = 0;
+  c->detail = 0;
+  c->asset_dir = nullptr;
+  return FR_OK;
+}
+
+const char* fr_last_error(fr_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int fr_preset_camera(int scene, float eye[3], float target[3]) {
+  f3 e, t;
+  preset_camera(scene, e, t);
+  eye[0] = e.x; eye[1] = e.y; eye[2] = e.z;
+  target[0] = t.x; target[1] = t.y; target[2] = t.z;
+  return FR_OK;
+}
+
+int fr_camera_look_at(fr_camera_pose* pose, const float target[3], const float up[3]) {
+  if (!pose || !target) return FR_E_INVALID;
+  f3 pos = mk3(pose->pos[0], pose->pos[1], pose->pos[2]);
+  f3 tg = mk3(target[0], target[1], target[2]);
+  f3 u = up ? mk3(up[0], up[1], up[2]) : mk3(0, 1, 0);
+  f3 z = normalize(pos - tg);
+  f3 x = normalize(cross(u, z));
+  f3 y = normalize(cross(z, x));
+  float m[3][3] = {{x.x, x.y, x.z}, {y.x, y.y, y.z}, {z.x, z.y, z.z}};
+  Q q = qnormalize(quat_cast(m));
+  pose->rot[0] = q.w; pose->rot[1] = q.x; pose->rot[2] = q.y; pose->rot[3] = q.z;
+  return FR_OK;
+}
+
+int fr_camera_matrices(const fr_camera_pose* pose, float view[16], float proj[16]) {
+  if (!pose) return FR_E_INVALID;
+  M4 V, P;
+  pose_matrices(pose, V, P);
+  if (view) to_rowmajor(V, view);
+  if (proj) to_rowmajor(P, proj);
+  return FR_OK;
+}
+
+int fr_camera_uniforms(const fr_camera_pose* cur, const fr_camera_pose* prev, int width, int height, fr_camera* out) {
+  if (!cur || !out || width <= 0 || height <= 0) return FR_E_INVALID;
+  if (!prev) prev = cur;
+  M4 V, P, PV, pV, pP, pPV;
+  pose_matrices(cur, V, P);
+  PV = glm_mul(P, V);
+  pose_matrices(prev, pV, pP);
+  pPV = glm_mul(pP, pV);
+  float rm[16];
+  to_rowmajor(PV, rm);
+  if (!invert_rowmajor(rm, out->inv_vp)) return FR_E_INVALID;
+  to_rowmajor(pPV, out->prev_vp);
+  for (int k = 0; k < 3; k++) { out->eye[k] = cur->pos[k]; out->prev_eye[k] = prev->pos[k]; }
+  Q q{cur->rot[0], cur->rot[1], cur->rot[2], cur->rot[3]};
+  f3 up = qrot(q, mk3(0, 1, 0));
+  out->up[0] = up.x; out->up[1] = up.y; out->up[2] = up.z;
+  f3 fr = qrot(q, mk3(0, 0, -1));
+  out->target[0] = cur->pos[0] + fr.x; out->target[1] = cur->pos[1] + fr.y; out->target[2] = cur->pos[2] + fr.z;
+  // g_gaze = (w/2, h/2) ints (FR/gui.cpp:34-35); gaze = (g_gaze.x, H - g_gaze.y) (FR/PathTracer.cpp:795)
+  out->gaze[0] = (float)(width / 2);
+  out->gaze[1] = (float)(height - height / 2);
+  return FR_OK;
+}
+
+int fr_create(const fr_config* cfg_in, fr_ctx** out) {
+  if (!out) return fail(nullptr, FR_E_INVALID, "out is NULL");
+  *out = nullptr;
+  fr_config cfg;
+  if (cfg_in) cfg = *cfg_in; else fr_config_default(&cfg);
+  if (cfg.width <= 0 || cfg.height <= 0 || (size_t)cfg.width * cfg.height > (1u << 30))
+    return fail(nullptr, FR_E_INVALID, "width/height out of range");
+  if (!(cfg.spp == 1 || cfg.spp == 2 || cfg.spp == 4 || cfg.spp == 8))
+    return fail(nullptr, FR_E_UNSUPPORTED, "spp must be 1, 2, 4 or 8");
+  if (cfg.mask_mode < 0 || cfg.mask_mode > 3) return fail(nullptr, FR_E_INVALID, "bad mask_mode");
+  if (cfg.scene < 0 || cfg.scene > 2) return fail(nullptr, FR_E_INVALID, "bad scene preset");
+  if (cfg.refraction_max_depth < 0 || cfg.refraction_max_depth > 100) return fail(nullptr, FR_E_INVALID, "bad refraction_max_depth");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(nullptr, FR_E_HIP, "no HIP device available");
+  if (cfg.device < 0 || cfg.device >= ndev) return fail(nullptr, FR_E_INVALID, "device ordinal out of range");
+
+  fr_ctx* c = new fr_ctx();
+  c->cfg = cfg;
+  c->asset_dir = cfg.asset_dir ? cfg.asset_dir : "assets";
+  c->cfg.asset_dir = nullptr;
+  c->W = cfg.width; c->H = cfg.height;
+  auto bail = [&](int code) { g_create_error = c->err; fr_destroy(c); return code; };
+  if (hipSetDevice(cfg.device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(FR_E_HIP); }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { c->err = "stream create failed"; return bail(FR_E_HIP); }
+  for (auto& e : c->ev) hipEventCreate(&e);
+
+  std::string err;
+  if (!build_preset_scene(cfg.scene, c->asset_dir, cfg.texture_mode, cfg.light_power, cfg.detail, c->scene, err)) {
+    c->err = "scene: " + err;
+    return bail(FR_E_IO);
+  }
+  build_bvh(c->scene, c->bvh);
+  const HostScene& s = c->scene;
+  const int nt = s.num_tris();
+  std::vector<TriShade> shade(nt);
+  for (int i = 0; i < nt; i++) {
+    TriShade& t = shade[i];
+    f3 n0 = s.nrm[3 * i], n1 = s.nrm[3 * i + 1], n2 = s.nrm[3 * i + 2];
+    f2 t0 = s.uv[3 * i], t1 = s.uv[3 * i + 1], t2 = s.uv[3 * i + 2];
+    t.n0 = mk4(n0, t0.x); t.n1 = mk4(n1, t0.y); t.n2 = mk4(n2, t1.x);
+    t.t = mk4(t1.y, t2.x, t2.y, bitsf((uint32_t)s.flags[i]));
+  }
+  auto up = [&](auto** dst, const auto& vec) -> bool {
+    using T = typename std::remove_reference<decltype(vec)>::type::value_type;
+    if (dalloc((T**)dst, vec.size()) != hipSuccess) return false;
+    return hipMemcpy(*dst, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!up(&c->d_nodes, c->bvh.nodes) || !up(&c->d_tri, c->bvh.tri_geo) || !up(&c->d_prim, c->bvh.tri_prim) ||
+      !up(&c->d_shade, shade)) {
+    c->err = "device allocation (scene) failed";
+    return bail(FR_E_NOMEM);
+  }
+  DevScene& d = c->dsc;
+  memset(&d, 0, sizeof(d));
+  d.nodes = c->d_nodes; d.tri_geo = c->d_tri; d.tri_prim = c->d_prim; d.shade = c->d_shade;
+  d.root_count = 0; d.num_tris = nt;
+  c->d_tex.resize(s.texs.size(), nullptr);
+  std::vector<DevTexture> htex(s.texs.size());
+  for (size_t i = 0; i < s.texs.size(); i++) {
+    if (!up(&c->d_tex[i], s.texs[i].data)) { c->err = "device allocation (texture) failed"; return bail(FR_E_NOMEM); }
+    htex[i] = DevTexture{c->d_tex[i], s.texs[i].w, s.texs[i].h};
+  }
+  if (!up(&c->d_mats, s.mats) || !up(&c->d_texs, htex)) { c->err = "device allocation (materials) failed"; return bail(FR_E_NOMEM); }
+  d.mats = c->d_mats;
+  d.texs = c->d_texs;
+  d.envmap = s.envmap;
+  d.light_position = s.light_position; d.light_v1 = s.light_v1; d.light_v2 = s.light_v2;
+  d.light_normal = s.light_normal; d.light_emission = s.light_emission;
+  d.light_area = length(cross(s.light_v1, s.light_v2));
+  d.bbox_min = s.bbox_min; d.bbox_max = s.bbox_max;
+  d.scene_epsilon = 1.e-3f;
+
+  const size_t N = (size_t)c->W * c->H;
+  for (int i = 0; i < P_COUNT; i++)
+    if (dalloc(&c->img[i], N) != hipSuccess) { c->err = "device allocation (images) failed"; return bail(FR_E_NOMEM); }
+  const size_t nwords = (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16) * 4;
+  c->pp_S = pp_size(c->W, c->H);
+  const size_t atlas = (size_t)c->pp_S * (c->pp_S + c->pp_S / 2);
+  if (dalloc(&c->mask, N) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
+      dalloc(&c->offsets, nwords) != hipSuccess || dalloc(&c->ray_count, 4) != hipSuccess ||
+      dalloc(&c->active, N) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
+      dalloc(&c->pull, atlas) != hipSuccess || dalloc(&c->push, atlas) != hipSuccess ||
+      dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess) {
+    c->err = "device allocation (work buffers) failed";
+    return bail(FR_E_NOMEM);
+  }
+  // Default camera: the preset pose, prev = current.
+  FrameUniforms& U = c->U;
+  memset(&U, 0, sizeof(U));
+  U.width = c->W; U.height = c->H;
+  U.screen = mk2((float)c->W, (float)c->H);
+  U.diffuse_max_depth = cfg.diffuse_max_depth;
+  U.reflection_max_depth = 4;
+  U.refraction_max_depth = cfg.refraction_max_depth;
+  U.spp = cfg.spp;
+  U.sqrt_spp = (int)floor(sqrt((double)cfg.spp) + 1e-9);
+  U.mask_mode = cfg.mask_mode;
+  {
+    fr_camera_pose pose;
+    float eye[3], tgt[3], upv[3] = {0, 1, 0};
+    fr_preset_camera(cfg.scene, eye, tgt);
+    memcpy(pose.pos, eye, sizeof(eye));
+    pose.rot[0] = 1; pose.rot[1] = pose.rot[2] = pose.rot[3] = 0;
+    pose.fovy_deg = 45.0f; pose.znear = 0.1f; pose.zfar = 500.1f;
+    pose.aspect = (float)c->W / (float)c->H;
+    fr_camera_look_at(&pose, tgt, upv);
+    fr_camera cam;
+    fr_camera_uniforms(&pose, &pose, c->W, c->H, &cam);
+    fr_set_camera(c, &cam);
+  }
+  if (hipDeviceSynchronize() != hipSuccess) { c->err = "device sync failed"; return bail(FR_E_HIP); }
+  *out = c;
+  return FR_OK;
+}
+
+int fr_destroy(fr_ctx* c) {
+  if (!c) return FR_E_INVALID;
+  hipSetDevice(c->cfg.device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  auto fr = [](void* p) { if (p) hipFree(p); };
+  fr(c->d_nodes); fr(c->d_tri); fr(c->d_prim); fr(c->d_shade);
+  for (auto p : c->d_tex) fr(p);
+  fr(c->d_mats); fr(c->d_texs);
+  for (auto p : c->img) fr(p);
+  fr(c->mask); fr(c->words); fr(c->offsets); fr(c->ray_count); fr(c->active); fr(c->jfa_a); fr(c->jfa_b);
+  fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats);
+  for (auto e : c->ev) if (e) hipEventDestroy(e);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return FR_OK;
+}
+
+int fr_set_camera(fr_ctx* c, const fr_camera* cam) {
+  if (!c || !cam) return FR_E_INVALID;
+  FrameUniforms& U = c->U;
+  memcpy(U.inv_vp.m, cam->inv_vp, sizeof(U.inv_vp.m));
+  memcpy(U.prev_vp.m, cam->prev_vp, sizeof(U.prev_vp.m));
+  U.eye = mk3(cam->eye[0], cam->eye[1], cam->eye[2]);
+  U.prev_eye = mk3(cam->prev_eye[0], cam->prev_eye[1], cam->prev_eye[2]);
+  U.gaze = mk2(cam->gaze[0], cam->gaze[1]);
+  return FR_OK;
+}
+
+int fr_set_light_power(fr_ctx* c, float power) {
+  if (!c) return FR_E_INVALID;
+  c->dsc.light_emission = mk3(power);
+  c->light_pending = true;
+  return FR_OK;
+}
+
+int fr_set_diffuse_max_depth(fr_ctx* c, int depth) {
+  if (!c || depth < 0) return FR_E_INVALID;
+  c->U.diffuse_max_depth = depth;
+  return FR_OK;
+}
+
+int fr_reset_accumulation(fr_ctx* c) {
+  if (!c) return FR_E_INVALID;
+  c->accum = 0;
+  return FR_OK;
+}
+
+int fr_accum_frame(fr_ctx* c, uint32_t* f) {
+  if (!c || !f) return FR_E_INVALID;
+  *f = c->accum;
+  return FR_OK;
+}
+
+static int enqueue_geometry(fr_ctx* c) {
+  // frame = m_accumFrame++ ; a light change resets the counter afterwards (FR/PathTracer.cpp:99-116)
+  c->U.frame = c->accum++;
+  if (c->light_pending) { c->light_pending = false; c->accum = 0; }
+  if (c->U.frame < 1) {  // d_buffer_init (g_buffer_trace_camera.cu:73-82)
+    const size_t bytes = (size_t)c->W * c->H * sizeof(f4);
+    hipMemsetAsync(c->img[c->hist_cur], 0, bytes, c->stream);
+    hipMemsetAsync(c->img[c->hist_cache], 0, bytes, c->stream);
+  }
+  launch_gbuffer(c->dsc, c->U, c->img[P_POSITION], c->img[P_NORMAL], c->img[c->depth_cur], c->img[P_DIFFUSE],
+                 c->img[P_WEIGHT], c->stats, c->stream);
+  c->compacted = false;
+  return check_launch(c);
+}
+
+static int enqueue_sampling(fr_ctx* c) {
+  c->mask_dirty = false;
+  launch_sampling(c->U, c->dsc, c->img[P_POSITION], c->img[c->depth_cur], c->img[c->depth_cache], c->img[P_WEIGHT],
+                  c->img[P_NORMAL], c->img[P_DIFFUSE], c->img[P_EXTRA], c->mask, c->words, c->cfg.write_extra,
+                  c->stream);
+  c->compacted = false;
+  return check_launch(c);
+}
+
+static int enqueue_optimize(fr_ctx* c) {
+  if (c->mask_dirty) {
+    launch_mask_words(c->mask, c->W, c->H, c->words, c->stream);
+    c->mask_dirty = false;
+  }
+  launch_compaction(c->W, c->H, c->words, c->offsets, c->ray_count, c->active, c->stream);
+  c->compacted = true;
+  return check_launch(c);
+}
+
+static int enqueue_shading(fr_ctx* c) {
+  if (!c->compacted) {  // g_isOptimize = 0: the active list is still needed by this design
+    int rc = enqueue_optimize(c);
+    if (rc) return rc;
+  }
+  launch_carry_history(c->U, c->mask, c->img[P_WEIGHT], c->img[c->hist_cache], c->img[c->hist_cur],
+                       c->img[P_SHADING], c->stream);
+  launch_shade(c->dsc, c->U, c->active, c->ray_count, (uint32_t)((size_t)c->W * c->H), c->img[P_WEIGHT],
+               c->img[c->hist_cache], c->img[c->hist_cur], c->img[P_SHADING], c->stats, c->stream);
+  int rc = check_launch(c);
+  // swapBuffer("history_cache", "history_buffer"); swapBuffer("depth_cache", "depth_buffer") (:226-227)
+  std::swap(c->hist_cur, c->hist_cache);
+  std::swap(c->depth_cur, c->depth_cache);
+  return rc;
+}
+
+static int resolve(fr_ctx* c, int id, int* phys) {
+  switch (id) {
+    case FR_BUF_POSITION: *phys = P_POSITION; return FR_OK;
+    case FR_BUF_NORMAL: *phys = P_NORMAL; return FR_OK;
+    case FR_BUF_DEPTH: *phys = c->depth_cur; return FR_OK;
+    case FR_BUF_DEPTH_CACHE: *phys = c->depth_cache; return FR_OK;
+    case FR_BUF_DIFFUSE: *phys = P_DIFFUSE; return FR_OK;
+    case FR_BUF_WEIGHT: *phys = P_WEIGHT; return FR_OK;
+    case FR_BUF_HISTORY: *phys = c->hist_cur; return FR_OK;
+    case FR_BUF_HISTORY_CACHE: *phys = c->hist_cache; return FR_OK;
+    case FR_BUF_SHADING: *phys = P_SHADING; return FR_OK;
+    case FR_BUF_EXTRA: *phys = P_EXTRA; return FR_OK;
+    case FR_BUF_JFA_COORD: *phys = P_JFA_COORD; return FR_OK;
+    case FR_BUF_JFA_COLOR: *phys = P_JFA_COLOR; return FR_OK;
+    case FR_BUF_SIBSON: *phys = P_SIBSON; return FR_OK;
+    case FR_BUF_PULLPUSH: *phys = P_PULLPUSH; return FR_OK;
+    case FR_BUF_ATROUS: *phys = c->atrous_out; return FR_OK;
+    default: return FR_E_INVALID;
+  }
+}
+
+static int enqueue_jfa(fr_ctx* c, int in_buffer) {
+  int p;
+  if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "jfa: bad input buffer");
+  launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->W, c->H, c->stream);
+  return check_launch(c);
+}
+static int enqueue_sibson(fr_ctx* c) {
+  launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, c->stream);
+  return check_launch(c);
+}
+static int enqueue_pullpush(fr_ctx* c, int in_buffer) {
+  int p;
+  if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "pullpush: bad input buffer");
+  launch_pullpush(c->img[p], c->pull, c->push, c->snap, c->img[P_PULLPUSH], c->W, c->H, c->stream);
+  return check_launch(c);
+}
+static int enqueue_atrous(fr_ctx* c, int count, int pos, int nrm, int col) {
+  int pp, pn, pc;
+  if (count < 1 || resolve(c, pos, &pp) || resolve(c, nrm, &pn) || resolve(c, col, &pc))
+    return fail(c, FR_E_INVALID, "atrous: bad arguments");
+  if (pc == P_ATROUS_A || pc == P_ATROUS_B) return fail(c, FR_E_INVALID, "atrous: colour input aliases the output");
+  float c_phi = 1.f, n_phi = 1.f, p_phi = 1.f;
+  int sw = 1;
+  launch_atrous(c->img[pp], c->img[pn], c->img[pc], c->img[P_ATROUS_A], c->W, c->H, c_phi, n_phi, p_phi, (float)sw, c->stream);
+  bool usingA = true;
+  for (int k = 1; k < count; k++) {  // FR/ATrous.cpp:90-113
+    c_phi *= 1.0f; n_phi *= 0.5f; p_phi *= 1.0f; sw *= 2;
+    if (usingA) launch_atrous(c->img[pp], c->img[pn], c->img[P_ATROUS_A], c->img[P_ATROUS_B], c->W, c->H, c_phi, n_phi, p_phi, (float)sw, c->stream);
+    else launch_atrous(c->img[pp], c->img[pn], c->img[P_ATROUS_B], c->img[P_ATROUS_A], c->W, c->H, c_phi, n_phi, p_phi, (float)sw, c->stream);
+    usingA = !usingA;
+  }
+  c->atrous_out = usingA ? P_ATROUS_A : P_ATROUS_B;
+  return check_launch(c);
+}
+
+static int timed(fr_ctx* c, const std::function<int()>& f, float* ms) {
+  hipSetDevice(c->cfg.device);
+  hipEventRecord(c->ev[0], c->stream);
+  int rc = f();
+  if (rc) return rc;
+  hipEventRecord(c->ev[1], c->stream);
+  hipError_t e = hipEventSynchronize(c->ev[1]);
+  if (e != hipSuccess) return fail(c, FR_E_HIP, std::string("stage failed: ") + hipGetErrorString(e));
+  if (ms) *ms = elapsed(c->ev[0], c->ev[1]);
+  return FR_OK;
+}
+
+int fr_geometry_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_geometry(c); }, ms); }
+int fr_sampling_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_sampling(c); }, ms); }
+int fr_optimize_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_optimize(c); }, ms); }
+int fr_shading_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_shading(c); }, ms); }
+
+static int ns_timed(fr_ctx* c, std::function<int()> f, uint64_t* ns) {
+  float ms = 0;
+  int rc = timed(c, f, &ms);
+  if (ns) *ns = (uint64_t)((double)ms * 1e6);
+  return rc;
+}
+int fr_jfa_render(fr_ctx* c, int in_buffer, uint64_t* ns) { if (!c) return FR_E_INVALID; return ns_timed(c, [&] { return enqueue_jfa(c, in_buffer); }, ns); }
+int fr_sibson_render(fr_ctx* c, uint64_t* ns) { if (!c) return FR_E_INVALID; return ns_timed(c, [&] { return enqueue_sibson(c); }, ns); }
+int fr_pullpush_render(fr_ctx* c, int in_buffer, uint64_t* ns) { if (!c) return FR_E_INVALID; return ns_timed(c, [&] { return enqueue_pullpush(c, in_buffer); }, ns); }
+int fr_atrous_render(fr_ctx* c, int count, int pos, int nrm, int col, uint64_t* ns) {
+  if (!c) return FR_E_INVALID;
+  return ns_timed(c, [&] { return enqueue_atrous(c, count, pos, nrm, col); }, ns);
+}
+
+int fr_frame(fr_ctx* c, fr_frame_timing* t) {
+  if (!c) return FR_E_INVALID;
+  hipSetDevice(c->cfg.device);
+  hipEvent_t* ev = c->ev;
+  if (t) hipEventRecord(ev[0], c->stream);
+  int rc;
+  if ((rc = enqueue_geometry(c))) return rc;
+  if (t) hipEventRecord(ev[1], c->stream);
+  if ((rc = enqueue_sampling(c))) return rc;
+  if (t) hipEventRecord(ev[2], c->stream);
+  if ((rc = enqueue_optimize(c))) return rc;
+  if (t) hipEventRecord(ev[3], c->stream);
+  if ((rc = enqueue_shading(c))) return rc;
+  if (t) hipEventRecord(ev[4], c->stream);
+  if ((rc = enqueue_jfa(c, FR_BUF_SHADING))) return rc;
+  if (t) hipEventRecord(ev[5], c->stream);
+  if ((rc = enqueue_sibson(c))) return rc;
+  if (t) hipEventRecord(ev[6], c->stream);
+  if ((rc = enqueue_pullpush(c, FR_BUF_SHADING))) return rc;
+  if (t) hipEventRecord(ev[7], c->stream);
+  if ((rc = enqueue_atrous(c, c->cfg.atrous_iterations, FR_BUF_POSITION, FR_BUF_NORMAL, FR_BUF_PULLPUSH))) return rc;
+  if (t) {
+    hipEventRecord(ev[8], c->stream);
+    hipError_t e = hipEventSynchronize(ev[8]);
+    if (e != hipSuccess) return fail(c, FR_E_HIP, std::string("frame failed: ") + hipGetErrorString(e));
+    t->geometry_ms = elapsed(ev[0], ev[1]);
+    t->sampling_ms = elapsed(ev[1], ev[2]);
+    t->optimize_ms = elapsed(ev[2], ev[3]);
+    t->shading_ms = elapsed(ev[3], ev[4]);
+    t->jfa_ms = elapsed(ev[4], ev[5]);
+    t->sibson_ms = elapsed(ev[5], ev[6]);
+    t->pullpush_ms = elapsed(ev[6], ev[7]);
+    t->atrous_ms = elapsed(ev[7], ev[8]);
+    t->total_ms = elapsed(ev[0], ev[8]);
+    hipMemcpy(&t->ray_count, c->ray_count, 4, hipMemcpyDeviceToHost);
+  }
+  return FR_OK;
+}
+
+int fr_synchronize(fr_ctx* c) {
+  if (!c) return FR_E_INVALID;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FR_OK;
+}
+
+int fr_ray_count(fr_ctx* c, uint32_t* n) {
+  if (!c || !n) return FR_E_INVALID;
+  HIP_TRY(c, hipMemcpyAsync(n, c->ray_count, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FR_OK;
+}
+
+int fr_gaze_target(fr_ctx* c, float xyz[3]) {
+  // gaze_target[0] = position_buffer[make_uint2(gaze)] (samplingStep.cu:184)
+  if (!c || !xyz) return FR_E_INVALID;
+  uint32_t gx = f2u_sat(c->U.gaze.x), gy = f2u_sat(c->U.gaze.y);
+  if (gx >= (uint32_t)c->W || gy >= (uint32_t)c->H) return fail(c, FR_E_STATE, "gaze outside the screen");
+  f4 v;
+  HIP_TRY(c, hipMemcpyAsync(&v, c->img[P_POSITION] + (size_t)gy * c->W + gx, sizeof(f4), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  xyz[0] = v.x; xyz[1] = v.y; xyz[2] = v.z;
+  return FR_OK;
+}
+
+int fr_get_buffer(fr_ctx* c, int id, fr_buffer_view* v) {
+  if (!c || !v) return FR_E_INVALID;
+  const size_t N = (size_t)c->W * c->H;
+  if (id == FR_BUF_THREAD) {
+    *v = fr_buffer_view{c->active, (int)N, 1, N * 4, N * 4, FR_FMT_U32};
+    return FR_OK;
+  }
+  if (id == FR_BUF_MASK) {
+    *v = fr_buffer_view{c->mask, c->W, c->H, (size_t)c->W, N, FR_FMT_U8};
+    return FR_OK;
+  }
+  int p;
+  if (resolve(c, id, &p)) return fail(c, FR_E_INVALID, "unknown buffer id");
+  *v = fr_buffer_view{c->img[p], c->W, c->H, (size_t)c->W * sizeof(f4), N * sizeof(f4), FR_FMT_RGBA32F};
+  return FR_OK;
+}
+
+int fr_read_buffer(fr_ctx* c, int id, void* host, size_t bytes) {
+  fr_buffer_view v;
+  int rc = fr_get_buffer(c, id, &v);
+  if (rc) return rc;
+  if (!host || bytes > v.bytes) return fail(c, FR_E_INVALID, "read_buffer: size");
+  HIP_TRY(c, hipMemcpyAsync(host, v.device_ptr, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FR_OK;
+}
+
+int fr_write_buffer(fr_ctx* c, int id, const void* host, size_t bytes) {
+  fr_buffer_view v;
+  int rc = fr_get_buffer(c, id, &v);
+  if (rc) return rc;
+  if (!host || bytes > v.bytes) return fail(c, FR_E_INVALID, "write_buffer: size");
+  HIP_TRY(c, hipMemcpyAsync(v.device_ptr, host, bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (id == FR_BUF_MASK) {
+    // a host-written mask must also drive the compaction: rebuild the wave ballots from it
+    c->compacted = false;
+    c->mask_dirty = true;
+  }
+  return FR_OK;
+}
+
+int fr_get_stats(fr_ctx* c, fr_stats* s) {
+  if (!c || !s) return FR_E_INVALID;
+  DevStats d;
+  HIP_TRY(c, hipMemcpyAsync(&d, c->stats, sizeof(d), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  s->gbuffer_primary = d.gbuffer_primary; s->primary = d.primary; s->shadow = d.shadow;
+  s->diffuse_bounce = d.diffuse_bounce; s->mirror = d.mirror; s->refraction = d.refraction;
+  s->reflection = d.reflection; s->truncated = d.truncated; s->overflow = d.bvh_overflow;
+  s->segments = d.gbuffer_primary + d.primary + d.shadow + d.diffuse_bounce + d.mirror + d.refraction + d.reflection;
+  return FR_OK;
+}
+
+int fr_reset_stats(fr_ctx* c) {
+  if (!c) return FR_E_INVALID;
+  HIP_TRY(c, hipMemsetAsync(c->stats, 0, sizeof(DevStats), c->stream));
+  return FR_OK;
+}
+
+int fr_scene_export(fr_ctx* c, fr_scene_arrays* o) {
+  if (!c || !o) return FR_E_INVALID;
+  const HostScene& s = c->scene;
+  memset(o, 0, sizeof(*o));
+  o->num_tris = s.num_tris();
+  o->pos = &s.pos[0].x; o->nrm = &s.nrm[0].x; o->uv = &s.uv[0].x; o->flags = s.flags.data();
+  c->mat_pairs.clear();
+  for (auto& m : s.mats) { c->mat_pairs.push_back(m.type); c->mat_pairs.push_back(m.tex); }
+  o->num_materials = (int)s.mats.size();
+  o->materials = c->mat_pairs.data();
+  c->tex_dims.clear(); c->tex_ptrs.clear();
+  for (auto& t : s.texs) { c->tex_dims.push_back(t.w); c->tex_dims.push_back(t.h); c->tex_ptrs.push_back(&t.data[0].x); }
+  o->num_textures = (int)s.texs.size();
+  o->tex_dims = c->tex_dims.data();
+  o->tex_data = c->tex_ptrs.data();
+  o->envmap = s.envmap;
+  const f3 L[5] = {s.light_position, s.light_v1, s.light_v2, s.light_normal, c->dsc.light_emission};
+  for (int i = 0; i < 5; i++) { o->light[3 * i] = L[i].x; o->light[3 * i + 1] = L[i].y; o->light[3 * i + 2] = L[i].z; }
+  o->bbox[0] = s.bbox_min.x; o->bbox[1] = s.bbox_min.y; o->bbox[2] = s.bbox_min.z;
+  o->bbox[3] = s.bbox_max.x; o->bbox[4] = s.bbox_max.y; o->bbox[5] = s.bbox_max.z;
+  o->bvh_nodes = (int)c->bvh.nodes.size();
+  o->bvh_depth = c->bvh.max_depth;
+  return FR_OK;
+}
+
+}  // extern "C"

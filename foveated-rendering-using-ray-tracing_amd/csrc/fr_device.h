@@ -1,0 +1,105 @@
+// fr_device.h — device-resident data layout of the fovrt hot path (shared by host builders and
+// the gfx950 kernels). Everything here is plain-old-data that lives in HBM for the lifetime of a
+// context; kernels receive the small descriptor structs by value.
+#pragma once
+#include "fr_math.h"
+
+namespace fr {
+
+enum MaterialType : int32_t { MATL_DIFFUSE = 0, MATL_REFLECTION = 1, MATL_REFRACTION = 2 };
+
+// Two-wide BVH node holding BOTH children's boxes (one 64-B line per node visit).
+// child[k] >= 0 with count[k] == 0  -> inner node index
+// count[k] > 0                      -> leaf: triangles [child[k], child[k]+count[k]) of tri_geo
+// count[k] < 0                      -> empty slot (never hit)
+struct alignas(16) BvhNode {
+  f4 bx;  // (c0.lo.x, c0.hi.x, c1.lo.x, c1.hi.x)
+  f4 by;  // (c0.lo.y, c0.hi.y, c1.lo.y, c1.hi.y)
+  f4 bz;  // (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
+  int32_t child[2];
+  int32_t count[2];
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode must be one 64-byte line");
+
+// Leaf-ordered triangle, pre-differenced exactly as optix::intersect_triangle does at run time
+// (e0 = p1 - p0, e1 = p0 - p2, n = cross(e1, e0); optixu_math_namespace.h, PTX
+// FR/cuda/triangle_mesh.ptx:380-430). Three 16-B loads per candidate triangle.
+struct alignas(16) TriGeo {
+  f4 a;  // p0.x p0.y p0.z e0.x
+  f4 b;  // e0.y e0.z e1.x e1.y
+  f4 c;  // e1.z n.x  n.y  n.z
+};
+
+// Per-primitive shading attributes, fetched once per closest hit (and per refractive any-hit).
+// flags = material index | (has_normals << 8) | (has_uv << 9)
+struct alignas(16) TriShade {
+  f4 n0;  // n0.xyz, t0.x
+  f4 n1;  // n1.xyz, t0.y
+  f4 n2;  // n2.xyz, t1.x
+  f4 t;   // t1.y, t2.x, t2.y, bits(flags)
+};
+#define FR_SHADE_HAS_NORMALS 0x100
+#define FR_SHADE_HAS_UV 0x200
+
+struct DevTexture {
+  const f4* data;  // row 0 = bottom (v = 0), RGBA, normalised float
+  int32_t w, h;
+};
+
+struct DevMaterial {
+  int32_t type;
+  int32_t tex;
+};
+
+#define FR_MAX_TEXTURES 8
+#define FR_MAX_MATERIALS 8
+
+struct DevScene {
+  const BvhNode* nodes;
+  const TriGeo* tri_geo;
+  const int32_t* tri_prim;  // leaf order -> original primitive index
+  const TriShade* shade;    // by original primitive index
+  int32_t root_count;       // >0: the whole scene is one leaf; else root is node 0
+  int32_t num_tris;
+  const DevMaterial* mats;  // device arrays (divergent indexing stays out of the kernarg segment)
+  const DevTexture* texs;
+  int32_t envmap;           // texture index of the lat-long environment map
+  // ParallelogramLight (FR/PathTracer.cpp:564-579)
+  f3 light_position, light_v1, light_v2, light_normal, light_emission;
+  float light_area;         // length(cross(v1, v2))
+  f3 bbox_min, bbox_max;
+  float scene_epsilon;      // 1e-3 (FR/PathTracer.cpp:474)
+};
+
+// Per-frame uniforms (FR/PathTracer.cpp:85-116, 774-820).
+struct FrameUniforms {
+  mat4 inv_vp;              // "mvp" on the device: inverse(P*V), row-major
+  mat4 prev_vp;             // "prev_mvp": P*V of the previous frame, row-major
+  f3 eye, prev_eye;
+  f2 gaze;                  // (g_gaze.x, H - g_gaze.y)
+  f2 screen;                // (W, H)
+  int32_t width, height;
+  uint32_t frame;           // m_accumFrame before the post-increment
+  int32_t diffuse_max_depth;
+  int32_t reflection_max_depth;   // 4 (FR/PathTracer.cpp:724)
+  int32_t refraction_max_depth;   // min(refraction_maxdepth=100, max_depth=100), capped
+  int32_t spp;
+  int32_t sqrt_spp;
+  int32_t mask_mode;
+};
+
+// Ray-segment statistics, accumulated with one atomic per wave.
+struct DevStats {
+  unsigned long long gbuffer_primary;
+  unsigned long long primary;
+  unsigned long long shadow;
+  unsigned long long diffuse_bounce;
+  unsigned long long mirror;
+  unsigned long long refraction;
+  unsigned long long reflection;
+  unsigned long long truncated;   // refraction nodes that hit the depth cap
+  unsigned long long bvh_overflow;
+  unsigned long long pad[7];
+};
+
+}  // namespace fr

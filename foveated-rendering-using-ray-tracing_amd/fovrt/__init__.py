@@ -1,0 +1,485 @@
+"""fovrt — Python mirror of the reference's renderer classes over the libfovrt C ABI.
+
+The reference drives its hot path from C++ (FR/main.cpp:152-462) through the classes
+``PathTracer``, ``JumpFlooding``, ``SibsonInterpolation``, ``PullPushInterpolation``, ``ATrous`` and
+``Camera``.  This module exposes the same names, method names and argument order on top of
+``include/fovrt.h`` (ctypes, no torch types), so tests and the benchmark read like the reference's
+frame loop.  GL texture handles become fr_buffer_id integers; ``get_texture`` returns the buffer id
+and ``read`` copies a buffer to a numpy array.
+
+Nothing here computes pixels: every stage runs in the HIP kernels of libfovrt.so.  Importing this
+module does not touch the GPU; creating a ``PathTracer`` does, and fails loudly (FovrtError) if the
+library or a device is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "libfovrt.so")
+REPO_ROOT = os.path.dirname(os.path.dirname(_PKG_DIR))
+DEFAULT_ASSET_DIR = os.path.join(REPO_ROOT, "assets")
+
+# fr_status
+FR_OK, FR_E_INVALID, FR_E_HIP, FR_E_NOMEM, FR_E_IO, FR_E_STATE, FR_E_UNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
+# scenes / masks
+SCENE_BOX, SCENE_BUNNY, SCENE_VOKSELIA = 0, 1, 2
+MASK_SALIENCY, MASK_LOGPOLAR, MASK_UNIFORM2X2, MASK_ALL = 0, 1, 2, 3
+SCENES = {"box": SCENE_BOX, "bunny": SCENE_BUNNY, "vokselia": SCENE_VOKSELIA}
+MASKS = {"saliency": MASK_SALIENCY, "logpolar": MASK_LOGPOLAR, "uniform": MASK_UNIFORM2X2, "all": MASK_ALL}
+
+
+class TextureName:
+    """PathTracer::TextureName (FR/PathTracer.h:13-31) plus the reconstruction outputs."""
+    POSITION, NORMAL, DEPTH, DIFFUSE, WEIGHT, THREAD, HISTORY, SHADING, EXTRA = range(9)
+    JFA_COORD, JFA_COLOR, SIBSON, PULLPUSH, ATROUS, DEPTH_CACHE, HISTORY_CACHE, MASK = range(9, 17)
+
+
+class FovrtError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"fovrt error {code}: {msg}")
+        self.code = code
+
+
+class fr_config(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("scene", C.c_int), ("mask_mode", C.c_int),
+                ("spp", C.c_int), ("diffuse_max_depth", C.c_int), ("refraction_max_depth", C.c_int),
+                ("light_power", C.c_float), ("optimize", C.c_int), ("atrous_iterations", C.c_int),
+                ("write_extra", C.c_int), ("device", C.c_int), ("texture_mode", C.c_int), ("detail", C.c_int),
+                ("asset_dir", C.c_char_p)]
+
+
+class fr_camera(C.Structure):
+    _fields_ = [("eye", C.c_float * 3), ("prev_eye", C.c_float * 3), ("inv_vp", C.c_float * 16),
+                ("prev_vp", C.c_float * 16), ("up", C.c_float * 3), ("target", C.c_float * 3),
+                ("gaze", C.c_float * 2)]
+
+
+class fr_camera_pose(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("rot", C.c_float * 4), ("fovy_deg", C.c_float),
+                ("znear", C.c_float), ("zfar", C.c_float), ("aspect", C.c_float)]
+
+
+class fr_buffer_view(C.Structure):
+    _fields_ = [("device_ptr", C.c_void_p), ("width", C.c_int), ("height", C.c_int),
+                ("pitch_bytes", C.c_size_t), ("bytes", C.c_size_t), ("format", C.c_int)]
+
+
+class fr_stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("gbuffer_primary", "primary", "shadow", "diffuse_bounce", "mirror",
+                                          "refraction", "reflection", "truncated", "overflow", "segments")]
+
+
+class fr_frame_timing(C.Structure):
+    _fields_ = [(n, C.c_float) for n in ("geometry_ms", "sampling_ms", "optimize_ms", "shading_ms", "jfa_ms",
+                                         "sibson_ms", "pullpush_ms", "atrous_ms", "total_ms")] + \
+               [("ray_count", C.c_uint32)]
+
+
+class fr_scene_arrays(C.Structure):
+    _fields_ = [("num_tris", C.c_int), ("pos", C.POINTER(C.c_float)), ("nrm", C.POINTER(C.c_float)),
+                ("uv", C.POINTER(C.c_float)), ("flags", C.POINTER(C.c_int32)), ("num_materials", C.c_int),
+                ("materials", C.POINTER(C.c_int32)), ("num_textures", C.c_int), ("tex_dims", C.POINTER(C.c_int32)),
+                ("tex_data", C.POINTER(C.POINTER(C.c_float))), ("envmap", C.c_int), ("light", C.c_float * 15),
+                ("bbox", C.c_float * 6), ("bvh_nodes", C.c_int), ("bvh_depth", C.c_int)]
+
+
+# exported symbols and their signatures (kept in sync with include/fovrt.h)
+_SIGS = {
+    "fr_config_default": [C.POINTER(fr_config)],
+    "fr_version": [],
+    "fr_create": [C.POINTER(fr_config), C.POINTER(C.c_void_p)],
+    "fr_destroy": [C.c_void_p],
+    "fr_last_error": [C.c_void_p],
+    "fr_camera_look_at": [C.POINTER(fr_camera_pose), C.POINTER(C.c_float), C.POINTER(C.c_float)],
+    "fr_camera_matrices": [C.POINTER(fr_camera_pose), C.POINTER(C.c_float), C.POINTER(C.c_float)],
+    "fr_camera_uniforms": [C.POINTER(fr_camera_pose), C.POINTER(fr_camera_pose), C.c_int, C.c_int,
+                           C.POINTER(fr_camera)],
+    "fr_preset_camera": [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float)],
+    "fr_set_camera": [C.c_void_p, C.POINTER(fr_camera)],
+    "fr_set_light_power": [C.c_void_p, C.c_float],
+    "fr_set_diffuse_max_depth": [C.c_void_p, C.c_int],
+    "fr_reset_accumulation": [C.c_void_p],
+    "fr_accum_frame": [C.c_void_p, C.POINTER(C.c_uint32)],
+    "fr_geometry_launch": [C.c_void_p, C.POINTER(C.c_float)],
+    "fr_sampling_launch": [C.c_void_p, C.POINTER(C.c_float)],
+    "fr_optimize_launch": [C.c_void_p, C.POINTER(C.c_float)],
+    "fr_shading_launch": [C.c_void_p, C.POINTER(C.c_float)],
+    "fr_ray_count": [C.c_void_p, C.POINTER(C.c_uint32)],
+    "fr_gaze_target": [C.c_void_p, C.POINTER(C.c_float)],
+    "fr_jfa_render": [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)],
+    "fr_sibson_render": [C.c_void_p, C.POINTER(C.c_uint64)],
+    "fr_pullpush_render": [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)],
+    "fr_atrous_render": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64)],
+    "fr_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
+    "fr_synchronize": [C.c_void_p],
+    "fr_get_buffer": [C.c_void_p, C.c_int, C.POINTER(fr_buffer_view)],
+    "fr_read_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
+    "fr_write_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
+    "fr_get_stats": [C.c_void_p, C.POINTER(fr_stats)],
+    "fr_reset_stats": [C.c_void_p],
+    "fr_scene_export": [C.c_void_p, C.POINTER(fr_scene_arrays)],
+}
+
+_lib = None
+
+
+def load_library(path: str | None = None):
+    """Loads libfovrt.so (raises FovrtError if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise FovrtError(FR_E_STATE, f"{path} not built: run __graft_entry__.build() or make -C "
+                                     f"foveated-rendering-using-ray-tracing_amd")
+    lib = C.CDLL(path)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_char_p if name in ("fr_version", "fr_last_error") else C.c_int
+    _lib = lib
+    return lib
+
+
+def _f(arr, n):
+    return (C.c_float * n)(*[float(v) for v in arr])
+
+
+# ------------------------------------------------------------------------------------------
+# Camera (FR/Camera.cpp): pose state on the host, matrices from the C ABI's glm restatement.
+# ------------------------------------------------------------------------------------------
+class Camera:
+    PM_Perspective = 0
+
+    def __init__(self):
+        self.pos = np.zeros(3, np.float32)
+        self.rot = np.array([1, 0, 0, 0], np.float32)  # glm::quat (w, x, y, z); FR/Camera.cpp:12 is (0,0,0,1) xyzw
+        self.fovy, self.znear, self.zfar = 45.0, 0.01, 100.0
+        self.aspect = 1.0
+        self.screen = (1, 1)
+        self.target = np.zeros(3, np.float32)
+        self.prev = None  # previous pose (setPrevState); None -> same as current
+
+    def setPosition(self, p):
+        self.pos = np.asarray(p, np.float32).copy()
+
+    def setRotation(self, q):
+        self.rot = np.asarray(q, np.float32).copy()
+
+    def setTarget(self, t):
+        self.target = np.asarray(t, np.float32).copy()
+
+    def setProjectMode(self, mode, fovy, n, f):
+        self.fovy, self.znear, self.zfar = float(fovy), float(n), float(f)
+
+    def setScreen(self, screen):
+        self.screen = (int(screen[0]), int(screen[1]))
+
+    def setViewport(self, vp):
+        self.aspect = np.float32(vp[2]) / np.float32(vp[3])
+
+    def lookAt(self, target, up=(0.0, 1.0, 0.0)):
+        lib = load_library()
+        pose = self._pose()
+        lib.fr_camera_look_at(C.byref(pose), _f(target, 3), _f(up, 3))
+        self.rot = np.array(pose.rot[:], np.float32)
+        self.target = np.asarray(target, np.float32).copy()
+
+    def _pose(self, which=None):
+        p = fr_camera_pose()
+        src = which or (self.pos, self.rot, self.fovy, self.znear, self.zfar, self.aspect)
+        p.pos[:] = [float(v) for v in src[0]]
+        p.rot[:] = [float(v) for v in src[1]]
+        p.fovy_deg, p.znear, p.zfar, p.aspect = float(src[2]), float(src[3]), float(src[4]), float(src[5])
+        return p
+
+    def getVMat(self):
+        return self._matrices()[0]
+
+    def getPMat(self):
+        return self._matrices()[1]
+
+    def _matrices(self):
+        lib = load_library()
+        v, p = (C.c_float * 16)(), (C.c_float * 16)()
+        lib.fr_camera_matrices(C.byref(self._pose()), v, p)
+        return np.array(v[:], np.float32).reshape(4, 4), np.array(p[:], np.float32).reshape(4, 4)
+
+    def setPrevState(self):
+        self.prev = (self.pos.copy(), self.rot.copy(), self.fovy, self.znear, self.zfar, self.aspect)
+
+    def uniforms(self, width, height) -> fr_camera:
+        lib = load_library()
+        cam = fr_camera()
+        cur = self._pose()
+        prev = self._pose(self.prev) if self.prev is not None else cur
+        rc = lib.fr_camera_uniforms(C.byref(cur), C.byref(prev), int(width), int(height), C.byref(cam))
+        if rc:
+            raise FovrtError(rc, "fr_camera_uniforms")
+        return cam
+
+    @staticmethod
+    def preset(scene, width, height):
+        """The reference's camera set-up (FR/main.cpp:179-209) for a scene preset."""
+        lib = load_library()
+        eye, tgt = (C.c_float * 3)(), (C.c_float * 3)()
+        lib.fr_preset_camera(int(scene), eye, tgt)
+        cam = Camera()
+        cam.setRotation((1, 0, 0, 0))
+        cam.setPosition(eye[:])
+        cam.lookAt(tgt[:])
+        cam.setProjectMode(Camera.PM_Perspective, 45, 0.1, 500.1)
+        cam.setScreen((width, height))
+        cam.setViewport((0, 0, width, height))
+        return cam
+
+
+@dataclass
+class Config:
+    width: int = 1024
+    height: int = 1024
+    scene: int = SCENE_BUNNY
+    mask_mode: int = MASK_SALIENCY
+    spp: int = 1
+    diffuse_max_depth: int = 1
+    refraction_max_depth: int = 16
+    light_power: float = 810.0
+    optimize: int = 1
+    atrous_iterations: int = 1
+    write_extra: int = 1
+    device: int = 0
+    texture_mode: int = 0
+    detail: int = 0
+    asset_dir: str = DEFAULT_ASSET_DIR
+
+    def to_c(self) -> fr_config:
+        c = fr_config()
+        for f in fr_config._fields_:
+            name = f[0]
+            if name == "asset_dir":
+                c.asset_dir = self.asset_dir.encode()
+            else:
+                setattr(c, name, getattr(self, name))
+        return c
+
+
+# ------------------------------------------------------------------------------------------
+# PathTracer (FR/PathTracer.h:73-94)
+# ------------------------------------------------------------------------------------------
+class PathTracer:
+    def __init__(self, config: Config | None = None):
+        self.config = config or Config()
+        self._ctx = None
+
+    # bool initialize(int w, int h)
+    def initialize(self, width=None, height=None):
+        if self._ctx is not None:
+            return False  # FR/PathTracer.cpp:43-45
+        lib = load_library()
+        if width is not None:
+            self.config.width, self.config.height = int(width), int(height)
+        self._cfg = self.config.to_c()  # keep asset_dir bytes alive
+        ctx = C.c_void_p()
+        rc = lib.fr_create(C.byref(self._cfg), C.byref(ctx))
+        if rc:
+            raise FovrtError(rc, lib.fr_last_error(None).decode())
+        self._ctx = ctx
+        return True
+
+    def __del__(self):
+        self.destroy()
+
+    def destroy(self):
+        if getattr(self, "_ctx", None) is not None and _lib is not None:
+            _lib.fr_destroy(self._ctx)
+            self._ctx = None
+
+    def _check(self, rc):
+        if rc:
+            raise FovrtError(rc, _lib.fr_last_error(self._ctx).decode())
+
+    @property
+    def width(self):
+        return self.config.width
+
+    @property
+    def height(self):
+        return self.config.height
+
+    def init_camera(self, camera: Camera):
+        self.update_optix_variables(camera)
+
+    def update_optix_variables(self, camera: Camera):
+        cam = camera.uniforms(self.width, self.height)
+        self._check(_lib.fr_set_camera(self._ctx, C.byref(cam)))
+
+    def set_camera_uniforms(self, cam: fr_camera):
+        self._check(_lib.fr_set_camera(self._ctx, C.byref(cam)))
+
+    def _launch(self, fn):
+        ms = C.c_float()
+        self._check(fn(self._ctx, C.byref(ms)))
+        return ms.value
+
+    def geometry_launch(self):
+        return self._launch(_lib.fr_geometry_launch)
+
+    def sampling_launch(self):
+        return self._launch(_lib.fr_sampling_launch)
+
+    def optimize_launch(self):
+        return self._launch(_lib.fr_optimize_launch)
+
+    def shading_launch(self):
+        return self._launch(_lib.fr_shading_launch)
+
+    @property
+    def m_accumFrame(self):
+        v = C.c_uint32()
+        self._check(_lib.fr_accum_frame(self._ctx, C.byref(v)))
+        return v.value
+
+    def reset_accumulation(self):
+        self._check(_lib.fr_reset_accumulation(self._ctx))
+
+    def set_light_power(self, p):
+        self._check(_lib.fr_set_light_power(self._ctx, float(p)))
+
+    def set_diffuse_max_depth(self, d):
+        self._check(_lib.fr_set_diffuse_max_depth(self._ctx, int(d)))
+
+    def ray_count(self):
+        v = C.c_uint32()
+        self._check(_lib.fr_ray_count(self._ctx, C.byref(v)))
+        return v.value
+
+    def gaze_target(self):
+        v = (C.c_float * 3)()
+        self._check(_lib.fr_gaze_target(self._ctx, v))
+        return np.array(v[:], np.float32)
+
+    def get_texture(self, name):
+        return int(name)
+
+    def view(self, buf) -> fr_buffer_view:
+        v = fr_buffer_view()
+        self._check(_lib.fr_get_buffer(self._ctx, int(buf), C.byref(v)))
+        return v
+
+    def read(self, buf) -> np.ndarray:
+        v = self.view(buf)
+        if v.format == 0:
+            out = np.empty((v.height, v.width, 4), np.float32)
+        elif v.format == 1:
+            out = np.empty((v.width,), np.uint32)
+        else:
+            out = np.empty((v.height, v.width), np.uint8)
+        self._check(_lib.fr_read_buffer(self._ctx, int(buf), out.ctypes.data, out.nbytes))
+        return out
+
+    def write(self, buf, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        self._check(_lib.fr_write_buffer(self._ctx, int(buf), arr.ctypes.data, arr.nbytes))
+
+    def stats(self) -> dict:
+        s = fr_stats()
+        self._check(_lib.fr_get_stats(self._ctx, C.byref(s)))
+        return {n: getattr(s, n) for n, _ in fr_stats._fields_}
+
+    def reset_stats(self):
+        self._check(_lib.fr_reset_stats(self._ctx))
+
+    def frame(self, timing=True):
+        """One iteration of the FR/main.cpp:253-358 loop body on the device."""
+        t = fr_frame_timing() if timing else None
+        self._check(_lib.fr_frame(self._ctx, C.byref(t) if timing else None))
+        if not timing:
+            return None
+        return {n: getattr(t, n) for n, _ in fr_frame_timing._fields_}
+
+    def synchronize(self):
+        self._check(_lib.fr_synchronize(self._ctx))
+
+    def scene_arrays(self) -> dict:
+        a = fr_scene_arrays()
+        self._check(_lib.fr_scene_export(self._ctx, C.byref(a)))
+        n = a.num_tris
+        tex = []
+        for i in range(a.num_textures):
+            w, h = a.tex_dims[2 * i], a.tex_dims[2 * i + 1]
+            tex.append(np.ctypeslib.as_array(a.tex_data[i], shape=(h, w, 4)).copy())
+        return {
+            "pos": np.ctypeslib.as_array(a.pos, shape=(n, 9)).copy(),
+            "nrm": np.ctypeslib.as_array(a.nrm, shape=(n, 9)).copy(),
+            "uv": np.ctypeslib.as_array(a.uv, shape=(n, 6)).copy(),
+            "flags": np.ctypeslib.as_array(a.flags, shape=(n,)).copy(),
+            "materials": np.ctypeslib.as_array(a.materials, shape=(a.num_materials, 2)).copy(),
+            "textures": tex,
+            "envmap": a.envmap,
+            "light": np.array(a.light[:], np.float32),
+            "bbox": np.array(a.bbox[:], np.float32),
+            "bvh_nodes": a.bvh_nodes,
+            "bvh_depth": a.bvh_depth,
+        }
+
+
+class _Pass:
+    def __init__(self, tracer: PathTracer):
+        self.tracer = tracer
+
+    def resetShader(self):  # GLSL reload (FR/JumpFlooding.cpp:51-58): nothing to reload here
+        pass
+
+
+class JumpFlooding(_Pass):
+    """JumpFlooding::render(rt, query, elapsed, done) (FR/JumpFlooding.cpp:60-140)."""
+    coordTex = TextureName.JFA_COORD
+    colorTex = TextureName.JFA_COLOR
+
+    def render(self, rt=TextureName.SHADING):
+        ns = C.c_uint64()
+        self.tracer._check(_lib.fr_jfa_render(self.tracer._ctx, int(rt), C.byref(ns)))
+        return ns.value
+
+
+class SibsonInterpolation(_Pass):
+    """SibsonInterpolation::render(coord, color, ...) (FR/SibsonInterpolation.cpp:28-53)."""
+    outputTex = TextureName.SIBSON
+
+    def render(self, coord=TextureName.JFA_COORD, color=TextureName.JFA_COLOR):
+        if coord != TextureName.JFA_COORD or color != TextureName.JFA_COLOR:
+            raise FovrtError(FR_E_UNSUPPORTED, "Sibson reads the JumpFlooding outputs")
+        ns = C.c_uint64()
+        self.tracer._check(_lib.fr_sibson_render(self.tracer._ctx, C.byref(ns)))
+        return ns.value
+
+
+class PullPushInterpolation(_Pass):
+    """PullPushInterpolation::render(sparse, ...) (FR/PullPushInterpolation.cpp:48-238)."""
+    outputTex = TextureName.PULLPUSH
+
+    def render(self, sparse=TextureName.SHADING):
+        ns = C.c_uint64()
+        self.tracer._check(_lib.fr_pullpush_render(self.tracer._ctx, int(sparse), C.byref(ns)))
+        return ns.value
+
+
+class ATrous(_Pass):
+    """ATrous::render(count, pos, nrm, col, rt, frame, ...) (FR/ATrous.cpp:47-132)."""
+    colorTex = TextureName.ATROUS
+
+    def render(self, count=1, positionTex=TextureName.POSITION, normalTex=TextureName.NORMAL,
+               colorTex=TextureName.PULLPUSH, rtTex=None, frame=0):
+        ns = C.c_uint64()
+        self.tracer._check(_lib.fr_atrous_render(self.tracer._ctx, int(count), int(positionTex), int(normalTex),
+                                                 int(colorTex), C.byref(ns)))
+        return ns.value
+
+
+def version():
+    return load_library().fr_version().decode()

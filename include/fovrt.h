@@ -1,0 +1,219 @@
+/* fovrt.h — C ABI of the MI355X-native foveated path-tracing + reconstruction engine.
+ *
+ * Drop-in boundary for the reference's hot path (ohseokkwon/Foveated-Rendering-using-Ray-Tracing).
+ * Every entry point replaces one call of the reference's frame loop (FR/main.cpp:253-358); the
+ * reference interface each one replaces is cited next to it ("FR/" = "Foveated Rendering using
+ * Ray Tracing/"). Conventions:
+ *   - every function returns FR_OK (0) or a negative fr_status; no exceptions cross the ABI;
+ *   - fr_last_error(ctx) (or fr_last_error(NULL) after a failed fr_create) describes the failure;
+ *   - the context owns all device memory (allocated in fr_create, freed in fr_destroy); per-frame
+ *     calls never allocate; views returned by fr_get_buffer are borrowed and stay valid until the
+ *     next call that writes that buffer, or fr_destroy;
+ *   - one context per device, one host thread per context (calls are serialised, not re-entrant);
+ *   - image buffers are row-major W x H with row 0 = bottom row (the OptiX launch index y and the
+ *     GL texture t of the reference agree on this), RGBA32F unless the view says otherwise.
+ */
+#ifndef FOVRT_H
+#define FOVRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FOVRT_ABI_VERSION 1
+
+typedef enum fr_status {
+  FR_OK = 0,
+  FR_E_INVALID = -1,     /* bad argument / unknown buffer id */
+  FR_E_HIP = -2,         /* HIP runtime error (no device, launch failure) */
+  FR_E_NOMEM = -3,       /* device allocation failed */
+  FR_E_IO = -4,          /* asset file missing or malformed */
+  FR_E_STATE = -5,       /* call out of order (e.g. shading before sampling) */
+  FR_E_UNSUPPORTED = -6  /* configuration outside what the engine implements */
+} fr_status;
+
+typedef enum fr_scene_preset {
+  FR_SCENE_BOX = 0,      /* ground + refractive box               (configs[0]) */
+  FR_SCENE_BUNNY = 1,    /* ground + box + bunny + reflective earth (configs[1], configs[2]) */
+  FR_SCENE_VOKSELIA = 2  /* all five models of FR/PathTracer.cpp:582-595 */
+} fr_scene_preset;
+
+typedef enum fr_mask_mode {
+  FR_MASK_SALIENCY = 0,   /* masked_sampling (FR/cuda/samplingStep.cu:222), the reference default */
+  FR_MASK_LOGPOLAR = 1,   /* log-polar round trip (FR/cuda/samplingStep.cu:180-182) */
+  FR_MASK_UNIFORM2X2 = 2, /* x%2==0 && y%2==0 (FR/PathTracer.cpp:526-533), non-foveated */
+  FR_MASK_ALL = 3         /* every pixel traced */
+} fr_mask_mode;
+
+typedef struct fr_config {
+  int width, height;          /* FR/main.cpp:127-135 (argv W H), default 1024 x 1024 */
+  int scene;                  /* fr_scene_preset */
+  int mask_mode;              /* fr_mask_mode */
+  int spp;                    /* 1, 2, 4 or 8 (reference: 1, FR/cuda/fov_path_trace_camera.cu:117) */
+  int diffuse_max_depth;      /* g_diffuse_max_depth (FR/gui.cpp:26), default 1 */
+  int refraction_max_depth;   /* min(refraction_maxdepth, max_depth) = 100 in the reference; default 16 */
+  float light_power;          /* g_light_Power (FR/gui.cpp:21), default 810 */
+  int optimize;               /* g_isOptimize (FR/gui.cpp:16): run the compaction (entry 2) */
+  int atrous_iterations;      /* ATrous::render count (FR/main.cpp:355), default 1 */
+  int write_extra;            /* write the saliency heat-map buffer (extra_buffer) */
+  int device;                 /* HIP device ordinal */
+  int texture_mode;           /* 0: reference assets from asset_dir (error if missing); 1: procedural */
+  int detail;                 /* procedural mesh detail (0 = preset default) */
+  const char* asset_dir;      /* directory holding CedarCity.hdr, grid.ppm, bunny/bunny.PPM, ... */
+} fr_config;
+
+/* Per-frame camera uniforms (PathTracer::update_optix_variables, FR/PathTracer.cpp:774-820).
+ * Matrices are row-major "math" matrices: v' = M v. */
+typedef struct fr_camera {
+  float eye[3];
+  float prev_eye[3];
+  float inv_vp[16];   /* device "mvp"      = inverse(P * V)           (:786-787) */
+  float prev_vp[16];  /* device "prev_mvp" = P * V of the previous frame (:789-790) */
+  float up[3];
+  float target[3];
+  float gaze[2];      /* (g_gaze.x, H - g_gaze.y) */
+} fr_camera;
+
+/* glm-style camera pose (FR/Camera.cpp): position, unit quaternion (w, x, y, z), perspective. */
+typedef struct fr_camera_pose {
+  float pos[3];
+  float rot[4];       /* glm::quat (w, x, y, z) */
+  float fovy_deg;     /* 45 (FR/main.cpp:207) */
+  float znear, zfar;  /* 0.1, 500.1 */
+  float aspect;       /* viewport w / h */
+} fr_camera_pose;
+
+typedef enum fr_buffer_id {
+  /* PathTracer::TextureName order (FR/PathTracer.h:13-31) */
+  FR_BUF_POSITION = 0,
+  FR_BUF_NORMAL = 1,
+  FR_BUF_DEPTH = 2,
+  FR_BUF_DIFFUSE = 3,
+  FR_BUF_WEIGHT = 4,
+  FR_BUF_THREAD = 5,        /* compacted active-pixel list (u32 pixel index, ray_count entries) */
+  FR_BUF_HISTORY = 6,
+  FR_BUF_SHADING = 7,
+  FR_BUF_EXTRA = 8,
+  /* reconstruction outputs (JumpFlooding / Sibson / PullPush / ATrous GL textures) */
+  FR_BUF_JFA_COORD = 9,
+  FR_BUF_JFA_COLOR = 10,
+  FR_BUF_SIBSON = 11,
+  FR_BUF_PULLPUSH = 12,
+  FR_BUF_ATROUS = 13,
+  /* temporal state (OptiX ping-pong partners) */
+  FR_BUF_DEPTH_CACHE = 14,
+  FR_BUF_HISTORY_CACHE = 15,
+  FR_BUF_MASK = 16,         /* u8 usingRay per pixel */
+  FR_BUF_COUNT = 17
+} fr_buffer_id;
+
+typedef enum fr_format { FR_FMT_RGBA32F = 0, FR_FMT_U32 = 1, FR_FMT_U8 = 2 } fr_format;
+
+typedef struct fr_buffer_view {
+  void* device_ptr;
+  int width, height;   /* elements; THREAD: width = capacity, height = 1 */
+  size_t pitch_bytes;  /* bytes per row */
+  size_t bytes;        /* total bytes */
+  int format;          /* fr_format */
+} fr_buffer_view;
+
+typedef struct fr_stats {
+  uint64_t gbuffer_primary;   /* entry-0 camera rays */
+  uint64_t primary;           /* entry-3 camera rays (ray_count * spp) */
+  uint64_t shadow;            /* shadow rays (light samples) */
+  uint64_t diffuse_bounce;    /* diffuse GI bounces */
+  uint64_t mirror;            /* reflection-material mirror rays */
+  uint64_t refraction;        /* refraction-material transmitted rays */
+  uint64_t reflection;        /* refraction-material reflected rays */
+  uint64_t truncated;         /* refraction nodes cut by refraction_max_depth */
+  uint64_t overflow;          /* work items dropped (explicit stack full) */
+  uint64_t segments;          /* sum of all traced ray segments */
+} fr_stats;
+
+typedef struct fr_frame_timing {
+  /* stage names of PrintMSTimes (FR/main.cpp:260-358); milliseconds measured with HIP events */
+  float geometry_ms, sampling_ms, optimize_ms, shading_ms;
+  float jfa_ms, sibson_ms, pullpush_ms, atrous_ms;
+  float total_ms;
+  uint32_t ray_count;
+} fr_frame_timing;
+
+typedef struct fr_ctx fr_ctx;
+
+int fr_config_default(fr_config* cfg);
+const char* fr_version(void);
+
+/* PathTracer::initialize(w, h) (FR/PathTracer.cpp:41-78) + the renderer constructors
+ * (FR/main.cpp:152-159). */
+int fr_create(const fr_config* cfg, fr_ctx** out);
+int fr_destroy(fr_ctx* ctx);
+const char* fr_last_error(fr_ctx* ctx);
+
+/* Camera (FR/Camera.cpp): glm-compatible helpers. */
+int fr_camera_look_at(fr_camera_pose* pose, const float target[3], const float up[3]);  /* :73-83 */
+int fr_camera_matrices(const fr_camera_pose* pose, float view[16], float proj[16]);      /* :139-181, row-major */
+int fr_camera_uniforms(const fr_camera_pose* cur, const fr_camera_pose* prev, int width, int height,
+                       fr_camera* out);  /* update_optix_variables' host math, gaze = screen centre */
+int fr_preset_camera(int scene, float eye[3], float target[3]);  /* FR/main.cpp:189-209 */
+
+/* PathTracer::init_camera / update_optix_variables (FR/PathTracer.cpp:606-632, 774-820) */
+int fr_set_camera(fr_ctx* ctx, const fr_camera* cam);
+int fr_set_light_power(fr_ctx* ctx, float power);          /* g_light_changed path, :103-116 */
+int fr_set_diffuse_max_depth(fr_ctx* ctx, int depth);      /* :800-806 */
+int fr_reset_accumulation(fr_ctx* ctx);                    /* tracer->m_accumFrame = 0 (FR/main.cpp:248) */
+int fr_accum_frame(fr_ctx* ctx, uint32_t* frame);          /* public m_accumFrame */
+
+/* The four OptiX launches (FR/PathTracer.cpp:85-230). Synchronous; *ms = elapsed milliseconds. */
+int fr_geometry_launch(fr_ctx* ctx, float* ms);   /* entry 0 g_buffer_trace */
+int fr_sampling_launch(fr_ctx* ctx, float* ms);   /* entry 1 sampling_step */
+int fr_optimize_launch(fr_ctx* ctx, float* ms);   /* entry 2 warp_sort x3 -> ray_count */
+int fr_shading_launch(fr_ctx* ctx, float* ms);    /* entry 3 ray_trace + history/depth swaps */
+int fr_ray_count(fr_ctx* ctx, uint32_t* count);   /* m_context["ray_count"] read-back (FR/main.cpp:288-299) */
+int fr_gaze_target(fr_ctx* ctx, float xyz[3]);    /* m_context["gaze_target"] read-back (:278-287) */
+
+/* GL reconstruction passes; *elapsed_ns like GL_TIME_ELAPSED (NULL allowed). */
+int fr_jfa_render(fr_ctx* ctx, int in_buffer, uint64_t* elapsed_ns);            /* JumpFlooding::render */
+int fr_sibson_render(fr_ctx* ctx, uint64_t* elapsed_ns);                        /* SibsonInterpolation::render */
+int fr_pullpush_render(fr_ctx* ctx, int in_buffer, uint64_t* elapsed_ns);       /* PullPushInterpolation::render */
+int fr_atrous_render(fr_ctx* ctx, int count, int pos_buffer, int nrm_buffer, int col_buffer,
+                     uint64_t* elapsed_ns);                                     /* ATrous::render */
+
+/* The whole main.cpp loop body (update -> 0 -> 1 -> 2 -> 3 -> JFA -> SI -> PPI -> AT), enqueued on the
+ * context stream. timing may be NULL (no host synchronisation then; call fr_synchronize). */
+int fr_frame(fr_ctx* ctx, fr_frame_timing* timing);
+int fr_synchronize(fr_ctx* ctx);
+
+/* Buffer access (PathTracer::get_texture, FR/PathTracer.cpp:337-374; rtBufferMap). */
+int fr_get_buffer(fr_ctx* ctx, int id, fr_buffer_view* view);
+int fr_read_buffer(fr_ctx* ctx, int id, void* host, size_t bytes);
+int fr_write_buffer(fr_ctx* ctx, int id, const void* host, size_t bytes);
+
+int fr_get_stats(fr_ctx* ctx, fr_stats* stats);
+int fr_reset_stats(fr_ctx* ctx);
+
+/* Scene inspection (host copies owned by the context; valid until fr_destroy). */
+typedef struct fr_scene_arrays {
+  int num_tris;
+  const float* pos;      /* 9 floats per triangle (p0, p1, p2) */
+  const float* nrm;      /* 9 floats per triangle */
+  const float* uv;       /* 6 floats per triangle */
+  const int32_t* flags;  /* material | 0x100 has_normals | 0x200 has_uv */
+  int num_materials;
+  const int32_t* materials;  /* (type, texture) pairs: 0 diffuse, 1 reflection, 2 refraction */
+  int num_textures;
+  const int32_t* tex_dims;   /* (w, h) pairs */
+  const float* const* tex_data;  /* RGBA32F, row 0 = bottom */
+  int envmap;
+  float light[15];       /* position, v1, v2, normal, emission */
+  float bbox[6];         /* min, max */
+  int bvh_nodes, bvh_depth;
+} fr_scene_arrays;
+int fr_scene_export(fr_ctx* ctx, fr_scene_arrays* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FOVRT_H */
