@@ -728,28 +728,74 @@ int fr_reset_stats(fr_ctx* c) {
   return FR_OK;
 }
 
-int fr_scene_export(fr_ctx* c, fr_scene_arrays* o) {
-  if (!c || !o) return FR_E_INVALID;
-  const HostScene& s = c->scene;
+}  // extern "C"
+
+struct fr_scene {
+  HostScene scene;
+  Bvh bvh;
+  std::string err;
+  std::vector<const float*> tex_ptrs;
+  std::vector<int32_t> tex_dims, mat_pairs;
+};
+
+static void fill_arrays(const HostScene& s, const Bvh& bvh, f3 emission, std::vector<int32_t>& mat_pairs,
+                        std::vector<int32_t>& tex_dims, std::vector<const float*>& tex_ptrs, fr_scene_arrays* o) {
   memset(o, 0, sizeof(*o));
   o->num_tris = s.num_tris();
   o->pos = &s.pos[0].x; o->nrm = &s.nrm[0].x; o->uv = &s.uv[0].x; o->flags = s.flags.data();
-  c->mat_pairs.clear();
-  for (auto& m : s.mats) { c->mat_pairs.push_back(m.type); c->mat_pairs.push_back(m.tex); }
+  mat_pairs.clear();
+  for (auto& m : s.mats) { mat_pairs.push_back(m.type); mat_pairs.push_back(m.tex); }
   o->num_materials = (int)s.mats.size();
-  o->materials = c->mat_pairs.data();
-  c->tex_dims.clear(); c->tex_ptrs.clear();
-  for (auto& t : s.texs) { c->tex_dims.push_back(t.w); c->tex_dims.push_back(t.h); c->tex_ptrs.push_back(&t.data[0].x); }
+  o->materials = mat_pairs.data();
+  tex_dims.clear(); tex_ptrs.clear();
+  for (auto& t : s.texs) { tex_dims.push_back(t.w); tex_dims.push_back(t.h); tex_ptrs.push_back(&t.data[0].x); }
   o->num_textures = (int)s.texs.size();
-  o->tex_dims = c->tex_dims.data();
-  o->tex_data = c->tex_ptrs.data();
+  o->tex_dims = tex_dims.data();
+  o->tex_data = tex_ptrs.data();
   o->envmap = s.envmap;
-  const f3 L[5] = {s.light_position, s.light_v1, s.light_v2, s.light_normal, c->dsc.light_emission};
+  const f3 L[5] = {s.light_position, s.light_v1, s.light_v2, s.light_normal, emission};
   for (int i = 0; i < 5; i++) { o->light[3 * i] = L[i].x; o->light[3 * i + 1] = L[i].y; o->light[3 * i + 2] = L[i].z; }
   o->bbox[0] = s.bbox_min.x; o->bbox[1] = s.bbox_min.y; o->bbox[2] = s.bbox_min.z;
   o->bbox[3] = s.bbox_max.x; o->bbox[4] = s.bbox_max.y; o->bbox[5] = s.bbox_max.z;
-  o->bvh_nodes = (int)c->bvh.nodes.size();
-  o->bvh_depth = c->bvh.max_depth;
+  o->bvh_nodes = (int)bvh.nodes.size();
+  o->bvh_depth = bvh.max_depth;
+}
+
+extern "C" {
+
+int fr_scene_export(fr_ctx* c, fr_scene_arrays* o) {
+  if (!c || !o) return FR_E_INVALID;
+  fill_arrays(c->scene, c->bvh, c->dsc.light_emission, c->mat_pairs, c->tex_dims, c->tex_ptrs, o);
+  return FR_OK;
+}
+
+int fr_scene_create(const fr_config* cfg_in, fr_scene** out) {
+  if (!out) return fail(nullptr, FR_E_INVALID, "out is NULL");
+  *out = nullptr;
+  fr_config cfg;
+  if (cfg_in) cfg = *cfg_in; else fr_config_default(&cfg);
+  if (cfg.scene < 0 || cfg.scene > 2) return fail(nullptr, FR_E_INVALID, "bad scene preset");
+  fr_scene* sc = new fr_scene();
+  std::string err;
+  if (!build_preset_scene(cfg.scene, cfg.asset_dir ? cfg.asset_dir : "assets", cfg.texture_mode, cfg.light_power,
+                          cfg.detail, sc->scene, err)) {
+    delete sc;
+    return fail(nullptr, FR_E_IO, "scene: " + err);
+  }
+  build_bvh(sc->scene, sc->bvh);
+  *out = sc;
+  return FR_OK;
+}
+
+int fr_scene_get_arrays(fr_scene* sc, fr_scene_arrays* o) {
+  if (!sc || !o) return FR_E_INVALID;
+  fill_arrays(sc->scene, sc->bvh, sc->scene.light_emission, sc->mat_pairs, sc->tex_dims, sc->tex_ptrs, o);
+  return FR_OK;
+}
+
+int fr_scene_destroy(fr_scene* sc) {
+  if (!sc) return FR_E_INVALID;
+  delete sc;
   return FR_OK;
 }
 

@@ -123,6 +123,9 @@ _SIGS = {
     "fr_get_stats": [C.c_void_p, C.POINTER(fr_stats)],
     "fr_reset_stats": [C.c_void_p],
     "fr_scene_export": [C.c_void_p, C.POINTER(fr_scene_arrays)],
+    "fr_scene_create": [C.POINTER(fr_config), C.POINTER(C.c_void_p)],
+    "fr_scene_get_arrays": [C.c_void_p, C.POINTER(fr_scene_arrays)],
+    "fr_scene_destroy": [C.c_void_p],
 }
 
 _lib = None
@@ -408,6 +411,10 @@ class PathTracer:
     def scene_arrays(self) -> dict:
         a = fr_scene_arrays()
         self._check(_lib.fr_scene_export(self._ctx, C.byref(a)))
+        return _arrays_to_dict(a)
+
+
+def _arrays_to_dict(a: fr_scene_arrays) -> dict:
         n = a.num_tris
         tex = []
         for i in range(a.num_textures):
@@ -426,6 +433,31 @@ class PathTracer:
             "bvh_nodes": a.bvh_nodes,
             "bvh_depth": a.bvh_depth,
         }
+
+
+class Scene:
+    """Host-only preset scene (fr_scene_create): no device required."""
+
+    def __init__(self, config: Config):
+        lib = load_library()
+        self._cfg = config.to_c()
+        h = C.c_void_p()
+        rc = lib.fr_scene_create(C.byref(self._cfg), C.byref(h))
+        if rc:
+            raise FovrtError(rc, lib.fr_last_error(None).decode())
+        self._h = h
+
+    def arrays(self) -> dict:
+        a = fr_scene_arrays()
+        rc = _lib.fr_scene_get_arrays(self._h, C.byref(a))
+        if rc:
+            raise FovrtError(rc, "fr_scene_get_arrays")
+        return _arrays_to_dict(a)
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None and _lib is not None:
+            _lib.fr_scene_destroy(self._h)
+            self._h = None
 
 
 class _Pass:

@@ -213,6 +213,13 @@ typedef struct fr_scene_arrays {
 } fr_scene_arrays;
 int fr_scene_export(fr_ctx* ctx, fr_scene_arrays* out);
 
+/* Host-only scene construction (no device needed): the same presets fr_create builds, for
+ * inspection, asset checks and CPU-side validation. */
+typedef struct fr_scene fr_scene;
+int fr_scene_create(const fr_config* cfg, fr_scene** out);
+int fr_scene_get_arrays(fr_scene* scene, fr_scene_arrays* out);
+int fr_scene_destroy(fr_scene* scene);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,123 @@
+"""CPU suite: the oracle against independent restatements, known-answer tests and golden fixtures.
+
+The reference ships no tests or fixtures and cannot run here, so the oracle is
+pinned by (1) hand-derived known answers, (2) independent pure-Python / numpy restatements of the
+same reference files, (3) brute-force ray casting, and (4) the committed golden vectors that the
+GPU path is also held to (tests/golden/make_golden.py regenerates them).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN, equal_nan, jfa_np, logpolar_mask_np, rnd_py, sparse_image, tea16_py
+
+
+def test_tea16_matches_python(oracle):
+    for a, b in [(0, 0), (1, 0), (12345, 7), (0xFFFFFFFF, 0xFFFFFFFF), (3840 * 1080 + 1920, 41)]:
+        assert oracle.tea16(a, b) == tea16_py(a, b)
+
+
+def test_rnd_sequence_matches_python(oracle):
+    for seed in (0, 1, 0xDEADBEEF, oracle.tea16(77, 3)):
+        ref, _ = rnd_py(seed, 16)
+        assert np.array_equal(oracle.rnd_seq(seed, 16), ref)
+    # rnd = lcg / 2^24 lies in [0, 1) and hits exactly 0 for lcg == 0
+    assert (oracle.rnd_seq(123, 1000) < 1.0).all()
+
+
+def test_tonemap_known_answers(oracle):
+    # Uncharted2ToneMapping (shared_helper_funcs.h:354-373): U(2c) / U(11.2), then pow 2.2.
+    f = np.float32
+
+    def U(x):
+        A, B, C, D, E, F = f(0.15), f(0.5), f(0.1), f(0.2), f(0.02), f(0.3)
+        return ((x * (A * x + C * B) + D * E) / (x * (A * x + B) + D * F)) - E / F
+
+    vals = np.array([[0.0, 0.1, 1.0], [10.0, 0.5, 2.0], [5.0, 5.0, 5.0]], np.float32)
+    ref = np.power(U(f(2.0) * vals) * (f(1.0) / U(f(11.2))), f(2.2), dtype=np.float32)
+    got = oracle.tonemap(vals)
+    assert np.allclose(got, ref, rtol=1e-6, atol=1e-7, equal_nan=True)
+    assert got[2, 0] == got[2, 1] == got[2, 2]
+    assert got[1, 0] > got[0, 2] > got[0, 1]  # monotone in the input
+    assert got[1, 0] > 1.0  # "gamma" is pow 2.2 (App. A #6): values above the white point exceed 1
+
+
+def test_oracle_bvh_equals_brute_force(oracle, fovrt_mod):
+    cfg = fovrt_mod.Config(scene=fovrt_mod.SCENE_BUNNY, texture_mode=1, detail=1)
+    a = fovrt_mod.Scene(cfg).arrays()
+    sc = oracle.OracleScene(a)
+    rng = np.random.default_rng(3)
+    n = 3000
+    o = rng.uniform(-4, 4, (n, 3)); o[:, 1] = rng.uniform(0.05, 3, n)
+    # aim half of the rays at the bunny / earth, half uniformly
+    tgt = np.where(rng.random((n, 1)) < 0.5, np.array([[-1.5, 0.7, 1.2]]), np.array([[0.0, 1.0, 0.0]]))
+    d = tgt + rng.normal(scale=0.3, size=(n, 3)) - o
+    d[: n // 4] = rng.normal(size=(n // 4, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d, np.full((n, 1), 1e-3), np.full((n, 1), np.inf)], 1).astype(np.float32)
+    A, B = sc.closest(rays), sc.closest(rays, brute=True)
+    assert (A[:, 1] >= 0).sum() > n // 3
+    assert np.array_equal(A, B)
+
+
+def test_oracle_jfa_matches_numpy_restatement(oracle):
+    W, H = 48, 40
+    rng = np.random.default_rng(5)
+    for density in (0.0, 0.02, 0.1, 1.0):
+        mask = (rng.random((H, W)) < density).astype(np.uint8)
+        img = sparse_image(W, H, mask)
+        c, col = oracle.jfa(img)
+        c2, col2 = jfa_np(img)
+        assert equal_nan(c, c2) and equal_nan(col, col2), density
+
+
+def test_logpolar_mask_matches_numpy_restatement(oracle, fovrt_mod):
+    W, H = 128, 96
+    cfg = fovrt_mod.Config(scene=fovrt_mod.SCENE_BOX, texture_mode=1)
+    sc = oracle.OracleScene(fovrt_mod.Scene(cfg).arrays())
+    cam = fovrt_mod.Camera.preset(fovrt_mod.SCENE_BOX, W, H).uniforms(W, H)
+    z = np.zeros((H, W, 4), np.float32)
+    out = oracle.sampling(sc, cam, W, H, 1, z, z, z, z, z, z)
+    ref = logpolar_mask_np(W, H, cam.gaze[0], cam.gaze[1])
+    assert np.array_equal(out["mask"], ref)
+    assert 0.05 < out["mask"].mean() < 0.3  # ~10% foveal density
+
+
+def test_warp_sort_permutation(oracle):
+    rng = np.random.default_rng(9)
+    for (W, H, p) in [(16, 8, 0.3), (33, 17, 0.05), (8, 8, 0.0), (8, 8, 1.0)]:
+        mask = (rng.random((H, W)) < p).astype(np.uint8)
+        n, tb = oracle.warp_sort(mask)
+        assert n == int(mask.sum())  # ray_count (warpSort.cu:76-82)
+        # a permutation of the pixels, with the active flag preserved (z > 0 <=> active)
+        xy = tb[..., :2].reshape(-1, 2)
+        assert len({(int(a), int(b)) for a, b in xy}) == W * H
+        act = tb[..., 2].reshape(-1) > 0
+        assert act.sum() == n
+        assert all(mask[int(b), int(a)] == 1 for (a, b), f in zip(xy, act) if f)
+
+
+@pytest.mark.parametrize("name", ["jfa_64x48", "pullpush_64", "sibson_64x48", "atrous_32", "logpolar_512", "kat"])
+def test_oracle_matches_golden(oracle, name):
+    path = os.path.join(GOLDEN, name + ".npz")
+    g = np.load(path)
+    if name.startswith("jfa"):
+        c, col = oracle.jfa(g["input"])
+        assert equal_nan(c, g["coord"]) and equal_nan(col, g["color"])
+    elif name.startswith("pullpush"):
+        st = oracle.PullPushState(g["inputs"].shape[2], g["inputs"].shape[1])
+        for k in range(g["inputs"].shape[0]):
+            assert equal_nan(st.render(g["inputs"][k]), g["outputs"][k]), k
+    elif name.startswith("sibson"):
+        assert equal_nan(oracle.sibson(g["coord"], g["color"]), g["output"])
+    elif name.startswith("atrous"):
+        out = oracle.atrous(int(g["count"]), g["pos"], g["nrm"], g["col"])
+        assert np.allclose(out, g["output"], rtol=0, atol=1e-6)
+    elif name.startswith("logpolar"):
+        H, W = g["mask"].shape
+        assert np.array_equal(logpolar_mask_np(W, H, float(g["gaze"][0]), float(g["gaze"][1])), g["mask"])
+    else:
+        assert [oracle.tea16(int(a), int(b)) for a, b in g["tea_in"]] == list(g["tea_out"])
+        assert np.array_equal(oracle.rnd_seq(int(g["rnd_seed"]), len(g["rnd_out"])), g["rnd_out"])
+        assert np.allclose(oracle.tonemap(g["tm_in"]), g["tm_out"], rtol=1e-6, atol=0)
