@@ -308,7 +308,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     return fail(nullptr, FR_E_INVALID, "width/height out of range");
   if (!(cfg.spp == 1 || cfg.spp == 2 || cfg.spp == 4 || cfg.spp == 8))
     return fail(nullptr, FR_E_UNSUPPORTED, "spp must be 1, 2, 4 or 8");
-  if (cfg.mask_mode < 0 || cfg.mask_mode > 3) return fail(nullptr, FR_E_INVALID, "bad mask_mode");
+  if (cfg.mask_mode < 0 || cfg.mask_mode > 4) return fail(nullptr, FR_E_INVALID, "bad mask_mode");
   if (cfg.scene < 0 || cfg.scene > 2) return fail(nullptr, FR_E_INVALID, "bad scene preset");
   if (cfg.refraction_max_depth < 0 || cfg.refraction_max_depth > 100) return fail(nullptr, FR_E_INVALID, "bad refraction_max_depth");
   int ndev = 0;

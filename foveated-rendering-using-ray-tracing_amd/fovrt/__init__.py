@@ -28,9 +28,10 @@ DEFAULT_ASSET_DIR = os.path.join(REPO_ROOT, "assets")
 FR_OK, FR_E_INVALID, FR_E_HIP, FR_E_NOMEM, FR_E_IO, FR_E_STATE, FR_E_UNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
 # scenes / masks
 SCENE_BOX, SCENE_BUNNY, SCENE_VOKSELIA = 0, 1, 2
-MASK_SALIENCY, MASK_LOGPOLAR, MASK_UNIFORM2X2, MASK_ALL = 0, 1, 2, 3
+MASK_SALIENCY, MASK_LOGPOLAR, MASK_UNIFORM2X2, MASK_ALL, MASK_LOGPOLAR_SIGNED = 0, 1, 2, 3, 4
 SCENES = {"box": SCENE_BOX, "bunny": SCENE_BUNNY, "vokselia": SCENE_VOKSELIA}
-MASKS = {"saliency": MASK_SALIENCY, "logpolar": MASK_LOGPOLAR, "uniform": MASK_UNIFORM2X2, "all": MASK_ALL}
+MASKS = {"saliency": MASK_SALIENCY, "logpolar": MASK_LOGPOLAR, "uniform": MASK_UNIFORM2X2, "all": MASK_ALL,
+         "logpolar10": MASK_LOGPOLAR_SIGNED}
 
 
 class TextureName:

@@ -45,7 +45,10 @@ typedef enum fr_mask_mode {
   FR_MASK_SALIENCY = 0,   /* masked_sampling (FR/cuda/samplingStep.cu:222), the reference default */
   FR_MASK_LOGPOLAR = 1,   /* log-polar round trip (FR/cuda/samplingStep.cu:180-182) */
   FR_MASK_UNIFORM2X2 = 2, /* x%2==0 && y%2==0 (FR/PathTracer.cpp:526-533), non-foveated */
-  FR_MASK_ALL = 3         /* every pixel traced */
+  FR_MASK_ALL = 3,        /* every pixel traced */
+  FR_MASK_LOGPOLAR_SIGNED = 4 /* log-polar round trip with signed pixel differences: the 10% foveal
+                               * density BASELINE.json quotes (the literal uint2 arithmetic of
+                               * samplingStep.cu:182 wraps negative differences, halving it) */
 } fr_mask_mode;
 
 typedef struct fr_config {

@@ -81,7 +81,11 @@ def test_logpolar_mask_matches_numpy_restatement(oracle, fovrt_mod):
     out = oracle.sampling(sc, cam, W, H, 1, z, z, z, z, z, z)
     ref = logpolar_mask_np(W, H, cam.gaze[0], cam.gaze[1])
     assert np.array_equal(out["mask"], ref)
-    assert 0.05 < out["mask"].mean() < 0.3  # ~10% foveal density
+    assert 0.03 < out["mask"].mean() < 0.08  # literal uint2 arithmetic: ~5% density
+    out = oracle.sampling(sc, cam, W, H, 4, z, z, z, z, z, z)
+    ref = logpolar_mask_np(W, H, cam.gaze[0], cam.gaze[1], signed=True)
+    assert np.array_equal(out["mask"], ref)
+    assert 0.09 < out["mask"].mean() < 0.13  # signed differences: the ~10% of SURVEY §8(a) row 5b
 
 
 def test_warp_sort_permutation(oracle):

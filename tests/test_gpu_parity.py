@@ -1,0 +1,252 @@
+"""GPU parity suite: every hot-path stage of libfovrt (HIP, gfx950) against the CPU oracle.
+
+Integer / index work and the fp32 image passes that contain no transcendental are held to bit
+equality; stages whose arithmetic goes through the platform fp32 libm (the materials' powf/cosf
+..., A-Trous expf) are held to the north-star tolerance (per-channel RMSE <= 1e-3) plus a tighter
+max-error bound. Each stage is fed the GPU's own upstream buffers, so a tolerance in one stage
+never leaks into the next stage's comparison.
+"""
+import numpy as np
+import pytest
+
+from helpers import (GOLDEN, TEXTURE_MODE, ASSET_DIR, equal_nan, logpolar_mask_np, rmse_per_channel,
+                     sparse_image)
+
+pytestmark = pytest.mark.gpu
+
+TN = None
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _tn(fovrt_mod):
+    global TN
+    TN = fovrt_mod.TextureName
+
+
+def make_tracer(fovrt, W, H, scene=1, mask=1, spp=1, dmd=1, refr=16):
+    t = fovrt.PathTracer(fovrt.Config(width=W, height=H, scene=scene, mask_mode=mask, spp=spp,
+                                      diffuse_max_depth=dmd, refraction_max_depth=refr,
+                                      texture_mode=TEXTURE_MODE, asset_dir=ASSET_DIR))
+    assert t.initialize()
+    return t
+
+
+def mismatch_report(a, b):
+    bad = ~np.isclose(a, b, rtol=0, atol=0, equal_nan=True)
+    if not bad.any():
+        return "equal"
+    idx = np.argwhere(bad)[:5]
+    return f"{bad.sum()} of {bad.size} differ; first {idx.tolist()}: gpu {a[tuple(idx[0])]} oracle {b[tuple(idx[0])]}"
+
+
+# ---------------------------------------------------------------------------------------------
+# entry 0 — G-buffer (bit-exact)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("scene", [0, 1, 2])
+def test_gbuffer_bit_exact(fovrt_mod, oracle, scene):
+    W, H = 96, 64
+    t = make_tracer(fovrt_mod, W, H, scene=scene)
+    uni = fovrt_mod.Camera.preset(scene, W, H).uniforms(W, H)
+    t.set_camera_uniforms(uni)
+    t.geometry_launch()
+    osc = oracle.OracleScene(t.scene_arrays())
+    ref = oracle.gbuffer(osc, uni, W, H, 0)
+    for name, tid in [("position", TN.POSITION), ("normal", TN.NORMAL), ("depth", TN.DEPTH),
+                      ("diffuse", TN.DIFFUSE), ("weight", TN.WEIGHT)]:
+        got = t.read(tid)
+        assert equal_nan(got, ref[name]), (name, mismatch_report(got, ref[name]))
+    assert t.stats()["gbuffer_primary"] == W * H
+
+
+# ---------------------------------------------------------------------------------------------
+# entries 1 + 2 — sampling mask (bit-exact), compaction / ray_count (bit-exact)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("mask_mode", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("scene", [1, 2])
+def test_sampling_and_compaction_bit_exact(fovrt_mod, oracle, scene, mask_mode):
+    W, H = 128, 96
+    t = make_tracer(fovrt_mod, W, H, scene=scene, mask=mask_mode)
+    uni = fovrt_mod.Camera.preset(scene, W, H).uniforms(W, H)
+    t.set_camera_uniforms(uni)
+    osc = oracle.OracleScene(t.scene_arrays())
+    for frame in range(2):  # frame 1 has a valid depth cache -> isValid / reprojection paths
+        t.geometry_launch()
+        inp = {k: t.read(v) for k, v in [("position", TN.POSITION), ("depth", TN.DEPTH), ("depth_cache", TN.DEPTH_CACHE),
+                                         ("weight", TN.WEIGHT), ("normal", TN.NORMAL), ("diffuse", TN.DIFFUSE)]}
+        t.sampling_launch()
+        ref = oracle.sampling(osc, uni, W, H, mask_mode, inp["position"], inp["depth"], inp["depth_cache"],
+                              inp["weight"], inp["normal"], inp["diffuse"])
+        mask = t.read(TN.MASK)
+        assert np.array_equal(mask, ref["mask"]), mismatch_report(mask, ref["mask"])
+        assert equal_nan(t.read(TN.WEIGHT), ref["weight"])
+        assert equal_nan(t.read(TN.EXTRA), ref["extra"]), mismatch_report(t.read(TN.EXTRA), ref["extra"])
+        t.optimize_launch()
+        n = t.ray_count()
+        n_ref, _ = oracle.warp_sort(mask)
+        assert n == n_ref == int(mask.sum())
+        lst = t.read(TN.THREAD)[:n]
+        assert np.array_equal(np.sort(lst), np.flatnonzero(mask.reshape(-1)))
+        t.shading_launch()
+    if mask_mode in (1, 4):
+        assert np.array_equal(mask, logpolar_mask_np(W, H, uni.gaze[0], uni.gaze[1], signed=mask_mode == 4))
+
+
+# ---------------------------------------------------------------------------------------------
+# entry 3 — foveated shading (north-star tolerance: per-channel RMSE <= 1e-3)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("scene,spp,dmd,mask_mode", [(0, 1, 1, 3), (1, 1, 1, 1), (1, 4, 3, 1), (1, 4, 3, 3),
+                                                     (2, 2, 3, 0), (2, 8, 1, 1)])
+def test_shading_within_tolerance(fovrt_mod, oracle, scene, spp, dmd, mask_mode):
+    W, H = 64, 48
+    t = make_tracer(fovrt_mod, W, H, scene=scene, mask=mask_mode, spp=spp, dmd=dmd)
+    uni = fovrt_mod.Camera.preset(scene, W, H).uniforms(W, H)
+    t.set_camera_uniforms(uni)
+    osc = oracle.OracleScene(t.scene_arrays(), refraction_max_depth=16, diffuse_max_depth=dmd)
+    for _ in range(3):
+        frame = t.m_accumFrame
+        t.geometry_launch()
+        t.sampling_launch()
+        t.optimize_launch()
+        mask, weight, hist_in = t.read(TN.MASK), t.read(TN.WEIGHT), t.read(TN.HISTORY_CACHE)
+        t.shading_launch()
+        got_sh, got_hist = t.read(TN.SHADING), t.read(TN.HISTORY_CACHE)  # swapped: cache = just written
+        ref = oracle.shading(osc, uni, W, H, frame, spp, mask, weight, hist_in)
+        rm = rmse_per_channel(got_sh, ref["shading"])
+        assert (rm <= 1e-3).all(), (frame, rm, mismatch_report(got_sh, ref["shading"]))
+        assert np.abs(np.nan_to_num(got_sh - ref["shading"], nan=1.0)).max() < 5e-2
+        exact = np.mean(np.all(got_sh == ref["shading"], axis=-1))
+        assert exact > 0.5, exact
+        # inactive pixels carry history exactly; alpha is exactly 0 or 1 (App. A #14)
+        inactive = mask == 0
+        assert equal_nan(got_hist[inactive], ref["history"][inactive])
+        assert set(np.unique(got_sh[..., 3]).tolist()) <= {0.0, 1.0}
+    st = t.stats()
+    assert st["overflow"] == 0 and st["primary"] > 0
+
+
+# ---------------------------------------------------------------------------------------------
+# JumpFlooding / Sibson / PullPush — bit-exact; A-Trous — tolerance
+# ---------------------------------------------------------------------------------------------
+def _box_tracer(fovrt_mod, W, H):
+    return make_tracer(fovrt_mod, W, H, scene=0, mask=3)
+
+
+JFA_CASES = [(64, 48, "logpolar"), (512, 512, "logpolar"), (1920, 1080, "logpolar"), (33, 17, 0.1),
+             (40, 40, 0.0), (40, 40, 1.0), (1, 1, 1.0), (7, 5, "single"), (256, 64, 0.003)]
+
+
+def _mask(W, H, kind, rng):
+    if kind == "logpolar":
+        return logpolar_mask_np(W, H, W // 2, H - H // 2)
+    if kind == "single":
+        m = np.zeros((H, W), np.uint8)
+        m[H // 3, W - 1] = 1
+        return m
+    return (rng.random((H, W)) < kind).astype(np.uint8)
+
+
+@pytest.mark.parametrize("W,H,kind", JFA_CASES)
+def test_jfa_and_sibson_bit_exact(fovrt_mod, oracle, W, H, kind):
+    rng = np.random.default_rng(W * 131 + H)
+    img = sparse_image(W, H, _mask(W, H, kind, rng), seed=W + H)
+    t = _box_tracer(fovrt_mod, W, H)
+    t.write(TN.SHADING, img)
+    fovrt_mod.JumpFlooding(t).render(TN.SHADING)
+    coord, color = t.read(TN.JFA_COORD), t.read(TN.JFA_COLOR)
+    rc, rcol = oracle.jfa(img)
+    assert equal_nan(coord, rc), mismatch_report(coord, rc)
+    assert equal_nan(color, rcol), mismatch_report(color, rcol)
+    if W * H <= 512 * 512:
+        fovrt_mod.SibsonInterpolation(t).render()
+        si = t.read(TN.SIBSON)
+        rs = oracle.sibson(rc, rcol)
+        assert equal_nan(si, rs), mismatch_report(si, rs)
+
+
+@pytest.mark.parametrize("W,H", [(64, 64), (96, 64), (256, 256), (130, 70)])
+def test_pullpush_bit_exact_across_frames(fovrt_mod, oracle, W, H):
+    rng = np.random.default_rng(W + 7 * H)
+    t = _box_tracer(fovrt_mod, W, H)
+    st = oracle.PullPushState(W, H)
+    for k, p in enumerate((0.1, 0.01, 0.3, 0.0)):
+        img = sparse_image(W, H, (rng.random((H, W)) < p).astype(np.uint8), seed=k)
+        t.write(TN.SHADING, img)
+        fovrt_mod.PullPushInterpolation(t).render(TN.SHADING)
+        got = t.read(TN.PULLPUSH)
+        ref = st.render(img)
+        assert equal_nan(got, ref), (k, mismatch_report(got, ref))
+
+
+@pytest.mark.parametrize("count", [1, 2, 3])
+def test_atrous_within_tolerance(fovrt_mod, oracle, count):
+    W, H = 80, 60
+    rng = np.random.default_rng(count)
+    t = _box_tracer(fovrt_mod, W, H)
+    pos, nrm, col = (rng.random((H, W, 4), dtype=np.float32) for _ in range(3))
+    t.write(TN.POSITION, pos)
+    t.write(TN.NORMAL, nrm)
+    t.write(TN.PULLPUSH, col)
+    fovrt_mod.ATrous(t).render(count, TN.POSITION, TN.NORMAL, TN.PULLPUSH)
+    got = t.read(TN.ATROUS)
+    ref = oracle.atrous(count, pos, nrm, col)
+    assert np.abs(got - ref).max() < 2e-6
+
+
+def test_golden_vectors_on_gpu(fovrt_mod):
+    import os
+    g = np.load(os.path.join(GOLDEN, "jfa_64x48.npz"))
+    t = _box_tracer(fovrt_mod, 64, 48)
+    t.write(TN.SHADING, g["input"])
+    fovrt_mod.JumpFlooding(t).render()
+    assert equal_nan(t.read(TN.JFA_COORD), g["coord"]) and equal_nan(t.read(TN.JFA_COLOR), g["color"])
+    s = np.load(os.path.join(GOLDEN, "sibson_64x48.npz"))
+    fovrt_mod.SibsonInterpolation(t).render()
+    assert equal_nan(t.read(TN.SIBSON), s["output"])
+    p = np.load(os.path.join(GOLDEN, "pullpush_64.npz"))
+    t2 = _box_tracer(fovrt_mod, 64, 64)
+    for k in range(p["inputs"].shape[0]):
+        t2.write(TN.SHADING, p["inputs"][k])
+        fovrt_mod.PullPushInterpolation(t2).render()
+        assert equal_nan(t2.read(TN.PULLPUSH), p["outputs"][k]), k
+
+
+# ---------------------------------------------------------------------------------------------
+# Whole frame: fr_frame == the reference's stage-by-stage call sequence; full-size properties
+# ---------------------------------------------------------------------------------------------
+def test_frame_driver_equals_stage_calls(fovrt_mod):
+    W, H = 128, 128
+    a = make_tracer(fovrt_mod, W, H, scene=1, mask=1, spp=4, dmd=3)
+    b = make_tracer(fovrt_mod, W, H, scene=1, mask=1, spp=4, dmd=3)
+    for _ in range(3):
+        a.frame(timing=True)
+        b.geometry_launch(); b.sampling_launch(); b.optimize_launch(); b.shading_launch()
+        fovrt_mod.JumpFlooding(b).render(TN.SHADING)
+        fovrt_mod.SibsonInterpolation(b).render()
+        fovrt_mod.PullPushInterpolation(b).render(TN.SHADING)
+        fovrt_mod.ATrous(b).render(1, TN.POSITION, TN.NORMAL, TN.PULLPUSH)
+    for tid in (TN.SHADING, TN.JFA_COLOR, TN.SIBSON, TN.PULLPUSH, TN.ATROUS, TN.HISTORY_CACHE):
+        assert equal_nan(a.read(tid), b.read(tid)), tid
+
+
+def test_full_size_frame_properties(fovrt_mod):
+    """BASELINE configs[2] at its full size (bunny, 3840x2160, 4 spp, GI 3, 10% log-polar mask):
+    size-independent invariants of every stage."""
+    W, H = 3840, 2160
+    t = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    for _ in range(2):
+        tm = t.frame(timing=True)
+    mask = t.read(TN.MASK)
+    n = t.ray_count()
+    assert n == tm["ray_count"] == int(mask.sum())
+    assert 0.08 < n / (W * H) < 0.12  # ~9.5% at 4K
+    assert np.array_equal(mask, logpolar_mask_np(W, H, W // 2, H - H // 2, signed=True))
+    sh = t.read(TN.SHADING)
+    assert np.all(sh[..., 3][mask == 1] == 1.0)
+    coord = t.read(TN.JFA_COORD)
+    assert np.all(coord[..., 3] == 1.0)  # every pixel found a seed
+    at = t.read(TN.ATROUS)
+    assert np.isfinite(at).mean() > 0.999
+    st = t.stats()
+    assert st["overflow"] == 0
+    assert st["primary"] == 2 * n * 4
+    assert st["gbuffer_primary"] == 2 * W * H
