@@ -18,15 +18,17 @@
 #include "scene.h"
 
 namespace fr {
-void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, DevStats*, hipStream_t);
+void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
 void launch_shade(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
                   const f4*, f4*, f4*, DevStats*, hipStream_t);
 void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
 void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
-                     const f4*, f4*, uint8_t*, unsigned long long*, int, hipStream_t);
-void launch_mask_words(const uint8_t*, int, int, unsigned long long*, hipStream_t);
-void launch_compaction(int, int, const unsigned long long*, uint32_t*, uint32_t*, uint32_t*, hipStream_t);
-void launch_jfa(const f4*, uint32_t*, uint32_t*, f4*, f4*, int, int, hipStream_t);
+                     const f4*, f4*, uint8_t*, const uint8_t*, unsigned long long*, uint32_t*, int, hipStream_t);
+void launch_mask_words(const uint8_t*, const uint8_t*, int, int, unsigned long long*, uint32_t*, hipStream_t);
+void launch_compaction(int, int, const unsigned long long*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
+                       uint32_t*, hipStream_t);
+size_t compaction_tiles(int W, int H);
+void launch_jfa(const f4*, uint32_t*, uint32_t*, float*, float*, f4*, f4*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
 void launch_pullpush(const f4*, f4*, f4*, f4*, f4*, int, int, hipStream_t);
 void launch_atrous(const f4*, const f4*, const f4*, f4*, int, int, float, float, float, float, hipStream_t);
@@ -66,11 +68,15 @@ struct fr_ctx {
   int hist_cur = P_HIST_A, hist_cache = P_HIST_B;
   int atrous_out = P_ATROUS_A;
   uint8_t* mask = nullptr;
+  uint8_t* gclass = nullptr;
   unsigned long long* words = nullptr;
-  uint32_t* offsets = nullptr;
+  uint32_t* counts = nullptr;
+  uint32_t* offsets = nullptr;  // per (class, block) local prefix
+  uint32_t* tiles = nullptr;
   uint32_t* ray_count = nullptr;
   uint32_t* active = nullptr;
   uint32_t *jfa_a = nullptr, *jfa_b = nullptr;
+  float *jfa_colx = nullptr, *jfa_coly = nullptr;
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
   int pp_S = 0;
   DevStats* stats = nullptr;
@@ -304,8 +310,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   *out = nullptr;
   fr_config cfg;
   if (cfg_in) cfg = *cfg_in; else fr_config_default(&cfg);
-  if (cfg.width <= 0 || cfg.height <= 0 || (size_t)cfg.width * cfg.height > (1u << 30))
-    return fail(nullptr, FR_E_INVALID, "width/height out of range");
+  if (cfg.width <= 0 || cfg.height <= 0 || cfg.width > 32767 || cfg.height > 32767)
+    return fail(nullptr, FR_E_INVALID, "width/height out of range (1..32767)");
   if (!(cfg.spp == 1 || cfg.spp == 2 || cfg.spp == 4 || cfg.spp == 8))
     return fail(nullptr, FR_E_UNSUPPORTED, "spp must be 1, 2, 4 or 8");
   if (cfg.mask_mode < 0 || cfg.mask_mode > 4) return fail(nullptr, FR_E_INVALID, "bad mask_mode");
@@ -374,12 +380,16 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   const size_t N = (size_t)c->W * c->H;
   for (int i = 0; i < P_COUNT; i++)
     if (dalloc(&c->img[i], N) != hipSuccess) { c->err = "device allocation (images) failed"; return bail(FR_E_NOMEM); }
-  const size_t nwords = (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16) * 4;
+  const size_t nblocks = (size_t)((c->W + 15) / 16) * ((c->H + 15) / 16);
+  const size_t nwords = nblocks * 16;  // 4 waves x 4 classes per 16x16 block
   c->pp_S = pp_size(c->W, c->H);
   const size_t atlas = (size_t)c->pp_S * (c->pp_S + c->pp_S / 2);
-  if (dalloc(&c->mask, N) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
-      dalloc(&c->offsets, nwords) != hipSuccess || dalloc(&c->ray_count, 4) != hipSuccess ||
+  if (compaction_tiles(c->W, c->H) > 1024) { c->err = "screen too large for the compaction scan"; return bail(FR_E_UNSUPPORTED); }
+  if (dalloc(&c->mask, N) != hipSuccess || dalloc(&c->gclass, N) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
+      dalloc(&c->counts, 4 * nblocks) != hipSuccess || dalloc(&c->offsets, 4 * nblocks) != hipSuccess ||
+      dalloc(&c->tiles, 1024) != hipSuccess || dalloc(&c->ray_count, 4) != hipSuccess ||
       dalloc(&c->active, N) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
+      dalloc(&c->jfa_colx, (size_t)c->W) != hipSuccess || dalloc(&c->jfa_coly, (size_t)c->H) != hipSuccess ||
       dalloc(&c->pull, atlas) != hipSuccess || dalloc(&c->push, atlas) != hipSuccess ||
       dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess) {
     c->err = "device allocation (work buffers) failed";
@@ -423,7 +433,7 @@ int fr_destroy(fr_ctx* c) {
   for (auto p : c->d_tex) fr(p);
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
-  fr(c->mask); fr(c->words); fr(c->offsets); fr(c->ray_count); fr(c->active); fr(c->jfa_a); fr(c->jfa_b);
+  fr(c->mask); fr(c->gclass); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->jfa_a); fr(c->jfa_b); fr(c->jfa_colx); fr(c->jfa_coly);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -477,7 +487,7 @@ static int enqueue_geometry(fr_ctx* c) {
     hipMemsetAsync(c->img[c->hist_cache], 0, bytes, c->stream);
   }
   launch_gbuffer(c->dsc, c->U, c->img[P_POSITION], c->img[P_NORMAL], c->img[c->depth_cur], c->img[P_DIFFUSE],
-                 c->img[P_WEIGHT], c->stats, c->stream);
+                 c->img[P_WEIGHT], c->gclass, c->stats, c->stream);
   c->compacted = false;
   return check_launch(c);
 }
@@ -485,18 +495,18 @@ static int enqueue_geometry(fr_ctx* c) {
 static int enqueue_sampling(fr_ctx* c) {
   c->mask_dirty = false;
   launch_sampling(c->U, c->dsc, c->img[P_POSITION], c->img[c->depth_cur], c->img[c->depth_cache], c->img[P_WEIGHT],
-                  c->img[P_NORMAL], c->img[P_DIFFUSE], c->img[P_EXTRA], c->mask, c->words, c->cfg.write_extra,
-                  c->stream);
+                  c->img[P_NORMAL], c->img[P_DIFFUSE], c->img[P_EXTRA], c->mask, c->gclass, c->words, c->counts,
+                  c->cfg.write_extra, c->stream);
   c->compacted = false;
   return check_launch(c);
 }
 
 static int enqueue_optimize(fr_ctx* c) {
   if (c->mask_dirty) {
-    launch_mask_words(c->mask, c->W, c->H, c->words, c->stream);
+    launch_mask_words(c->mask, c->gclass, c->W, c->H, c->words, c->counts, c->stream);
     c->mask_dirty = false;
   }
-  launch_compaction(c->W, c->H, c->words, c->offsets, c->ray_count, c->active, c->stream);
+  launch_compaction(c->W, c->H, c->words, c->counts, c->offsets, c->tiles, c->ray_count, c->active, c->stream);
   c->compacted = true;
   return check_launch(c);
 }
@@ -541,7 +551,7 @@ static int resolve(fr_ctx* c, int id, int* phys) {
 static int enqueue_jfa(fr_ctx* c, int in_buffer) {
   int p;
   if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "jfa: bad input buffer");
-  launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->W, c->H, c->stream);
+  launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->jfa_colx, c->jfa_coly, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->W, c->H, c->stream);
   return check_launch(c);
 }
 static int enqueue_sibson(fr_ctx* c) {
