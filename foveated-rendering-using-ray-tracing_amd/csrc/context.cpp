@@ -20,7 +20,8 @@
 namespace fr {
 void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
 void launch_shade(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
-                  const f4*, f4*, f4*, DevStats*, hipStream_t);
+                  const f4*, f4*, f4*, uint32_t*, f4*, DevStats*, hipStream_t);
+size_t shade_counter_words();
 void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
 void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
                      const f4*, f4*, uint8_t*, const uint8_t*, unsigned long long*, uint32_t*, int, hipStream_t);
@@ -75,6 +76,8 @@ struct fr_ctx {
   uint32_t* tiles = nullptr;
   uint32_t* ray_count = nullptr;
   uint32_t* active = nullptr;
+  uint32_t* shade_ctr = nullptr;  // sharded chunk counters of the shading work queue
+  f4* samples = nullptr;          // one radiance value per (active pixel, camera sample)
   uint32_t *jfa_a = nullptr, *jfa_b = nullptr;
   float *jfa_colx = nullptr, *jfa_coly = nullptr;
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
@@ -391,7 +394,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       dalloc(&c->active, N) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
       dalloc(&c->jfa_colx, (size_t)c->W) != hipSuccess || dalloc(&c->jfa_coly, (size_t)c->H) != hipSuccess ||
       dalloc(&c->pull, atlas) != hipSuccess || dalloc(&c->push, atlas) != hipSuccess ||
-      dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess) {
+      dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess ||
+      dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, N * cfg.spp) != hipSuccess) {
     c->err = "device allocation (work buffers) failed";
     return bail(FR_E_NOMEM);
   }
@@ -433,7 +437,7 @@ int fr_destroy(fr_ctx* c) {
   for (auto p : c->d_tex) fr(p);
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
-  fr(c->mask); fr(c->gclass); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->jfa_a); fr(c->jfa_b); fr(c->jfa_colx); fr(c->jfa_coly);
+  fr(c->mask); fr(c->gclass); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->jfa_a); fr(c->jfa_b); fr(c->jfa_colx); fr(c->jfa_coly);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -519,7 +523,8 @@ static int enqueue_shading(fr_ctx* c) {
   launch_carry_history(c->U, c->mask, c->img[P_WEIGHT], c->img[c->hist_cache], c->img[c->hist_cur],
                        c->img[P_SHADING], c->stream);
   launch_shade(c->dsc, c->U, c->active, c->ray_count, (uint32_t)((size_t)c->W * c->H), c->img[P_WEIGHT],
-               c->img[c->hist_cache], c->img[c->hist_cur], c->img[P_SHADING], c->stats, c->stream);
+               c->img[c->hist_cache], c->img[c->hist_cur], c->img[P_SHADING], c->shade_ctr, c->samples, c->stats,
+               c->stream);
   int rc = check_launch(c);
   // swapBuffer("history_cache", "history_buffer"); swapBuffer("depth_cache", "depth_buffer") (:226-227)
   std::swap(c->hist_cur, c->hist_cache);
