@@ -52,18 +52,19 @@ def jfa_passes(W, H):
 
 
 def cpu_baseline(args, cfg_scene_arrays, cam_uni_fn):
-    """The CPU oracle (oracle/, a literal restatement of the reference path) timed on this host on
-    a bounded sample: the same scene/spp/GI/mask at 1/4 x 1/4 resolution, second frame."""
+    """The CPU oracle (oracle/, a literal restatement of the reference path, OpenMP over rows) timed on
+    this host on a bounded sample: the full bench workload (same scene/resolution/spp/GI/mask), two
+    frames, the second one timed (frame 0 only establishes the temporal history)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
-    W, H = args.width // 4, args.height // 4
+    W, H = args.width // args.cpu_scale, args.height // args.cpu_scale
     sc = po.OracleScene(cfg_scene_arrays, refraction_max_depth=args.refraction_max_depth,
                         diffuse_max_depth=args.dmd)
     uni = cam_uni_fn(W, H)
     hist = np.zeros((H, W, 4), np.float32)
     depth_cache = np.zeros((H, W, 4), np.float32)
     pp = po.PullPushState(W, H)
-    t_total, segs = 0.0, 0
+    t_total, segs, t_all = 0.0, 0, time.perf_counter()
     for frame in range(2):
         sc.segments(reset=True)
         t0 = time.perf_counter()
@@ -81,11 +82,52 @@ def cpu_baseline(args, cfg_scene_arrays, cam_uni_fn):
         if frame == 1:
             t_total, segs = dt, sc.segments(reset=True)
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    scale = "" if args.cpu_scale == 1 else f" at 1/{args.cpu_scale} x 1/{args.cpu_scale} resolution"
     return {"value": round(segs / t_total / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "sample": f"oracle full frame at {W}x{H} (1/16 of the {args.width}x{args.height} workload), same "
-                      f"scene/spp/GI/mask, 2nd frame; {segs} ray segments counted as the reference traces "
-                      f"them (incl. rays whose results it never reads) in {t_total:.2f} s",
-            "frame_s": round(t_total, 3)}
+            "sample": f"oracle (OpenMP) full frame {W}x{H}{scale}, same scene/spp/GI/mask as the GPU workload; "
+                      f"frame 0 untimed (history), frame 1 timed: {segs} ray segments counted as the reference "
+                      f"traces them (incl. rays whose results it never reads) in {t_total:.2f} s "
+                      f"({time.perf_counter() - t_all:.1f} s of CPU work in total)",
+            "frame_s": round(t_total, 3), "fps": round(1.0 / t_total, 4)}
+
+
+def view_offset(rank, world):
+    """Weak scaling over views: rank r renders its own eye/view, offset along x by 6.4 cm per view
+    around the preset camera (the stereo pair of BASELINE configs[4] at world 2)."""
+    return np.array([0.064 * (rank - (world - 1) / 2.0), 0.0, 0.0], np.float32)
+
+
+def reduce_over_ranks(dist, device, elapsed, segs):
+    """Max of the elapsed times and sum of the ray segments over all ranks (value = all ranks' rays /
+    slowest rank's time)."""
+    import torch
+    if dist is None:
+        return elapsed, float(segs)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    s = torch.tensor([float(segs)], dtype=torch.float64, device=device)
+    dist.all_reduce(s, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(s.item())
+
+
+def load_traffic(kernels, config):
+    """HBM bytes per launch of `kernels` from the newest profiles/*_pmc_traffic.json recorded on the
+    same workload (scripts/profile.sh), else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        cfg = doc.get("config") or {}
+        if any(cfg.get(k) != config.get(k) for k in ("scene", "width", "height", "spp", "diffuse_max_depth",
+                                                     "mask_mode")):
+            continue
+        ks = doc.get("kernels", {})
+        if all(k in ks for k in kernels):
+            return sum(ks[k]["hbm_bytes"] for k in kernels), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def main():
@@ -101,6 +143,7 @@ def main():
     ap.add_argument("--dmd", type=int, default=3, help="diffuse_max_depth (GI bounces)")
     ap.add_argument("--refraction-max-depth", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-scale", type=int, default=1, help="CPU baseline at 1/scale resolution per axis")
     args = ap.parse_args()
     args.mask = fovrt.MASKS[args.mask]
     scene = fovrt.SCENES[args.scene]
@@ -135,7 +178,7 @@ def main():
     cam = fovrt.Camera.preset(scene, W, H)
     # weak scaling: rank r renders its own view (eye offset along x, 6.4 cm per view)
     if world > 1:
-        cam.setPosition(np.asarray(cam.pos) + np.array([0.064 * (rank - (world - 1) / 2.0), 0, 0], np.float32))
+        cam.setPosition(np.asarray(cam.pos) + view_offset(rank, world))
         cam.lookAt(cam.target)
     tracer.update_optix_variables(cam)
 
@@ -162,16 +205,10 @@ def main():
 
     st = tracer.stats()
     segs = st["segments"]
+    dev = None
     if dist is not None:
         dev = torch.device("cuda", local_rank) if has_gpu and dist.get_backend() == "nccl" else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        s = torch.tensor([float(segs)], dtype=torch.float64, device=dev)
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        total_segs = float(s.item())
-    else:
-        total_segs = float(segs)
+    elapsed, total_segs = reduce_over_ranks(dist, dev, elapsed, segs)
 
     K = args.steps
     avg = {k[:-3]: v / K for k, v in stage_ms.items()}
@@ -179,8 +216,12 @@ def main():
     L = jfa_passes(W, H)
     sb = stage_bytes(W, H, rho, args.spp, L)
     stage_table = {k: {"ms": round(avg[k], 4), "GB/s": round(sb[k] / (avg[k] * 1e-3) / 1e9, 1)} for k in sb}
+    # the dominant stage is entry 3 (shading_launch): k_shade_paths (path-trace megakernel) +
+    # k_shade_resolve + k_carry_history; its algorithmic bytes are SURVEY §8(d)'s (56 + 4 rho) B/px.
     dominant = max(sb, key=lambda k: avg[k])
     achieved = sb[dominant] / (avg[dominant] * 1e-3) / 1e9
+    stage_kernels = {"shading": ["k_shade_paths", "k_shade_resolve", "k_carry_history"],
+                     "geometry": ["k_gbuffer"], "sibson": ["k_sibson"]}
     image_stages = ["sampling", "optimize", "jfa", "sibson", "pullpush", "atrous"]
     img_bytes = sum(sb[k] for k in image_stages)
     img_ms = sum(avg[k] for k in image_stages)
@@ -209,15 +250,24 @@ def main():
         "rays": {k: st[k] for k in ("gbuffer_primary", "primary", "shadow", "diffuse_bounce", "mirror",
                                     "refraction", "reflection", "truncated", "overflow")},
         "stages": stage_table,
-        "roofline": {"bound": "hbm", "kernel": f"{dominant} stage", "achieved": round(achieved, 1),
-                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 5),
-                     "traffic": None,
-                     "note": "achieved = SURVEY §8(d) algorithmic bytes of the stage / its HIP-event duration; the "
-                             "trace stages are latency/divergence bound, image passes are HBM bound"},
+        "roofline": {"bound": "hbm", "kernel": f"{dominant} stage ({' + '.join(stage_kernels.get(dominant, []))})",
+                     "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": None,
+                     "ms_per_launch": round(avg[dominant], 4),
+                     "algorithmic_bytes_per_launch": int(sb[dominant]),
+                     "megakernel_ms": round(avg.get("shade_paths", 0.0), 4),
+                     "note": "achieved = SURVEY §8(d) algorithmic bytes of the stage / its HIP-event duration on the "
+                             "context stream; the path-trace megakernel is latency/divergence bound (BVH "
+                             "pointer chasing), so Mrays/s is its figure of merit, image passes are HBM bound"},
         "roofline_image_passes": {"bound": "hbm", "achieved": round(img_bytes / (img_ms * 1e-3) / 1e9, 1),
                                   "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                   "frac": round(img_bytes / (img_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)},
     }
+    traffic, src = load_traffic(stage_kernels.get(dominant, []), result["config"])
+    if traffic is not None:
+        result["roofline"]["traffic"] = int(traffic)
+        result["roofline"]["traffic_source"] = src
+        result["roofline"]["measured_hbm_GBs"] = round(traffic / (avg[dominant] * 1e-3) / 1e9, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             arrays = tracer.scene_arrays()

@@ -19,8 +19,10 @@
 
 namespace fr {
 void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
-void launch_shade(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
-                  const f4*, f4*, f4*, uint32_t*, f4*, DevStats*, hipStream_t);
+void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
+                        const f4*, uint32_t*, f4*, DevStats*, hipStream_t);
+void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
+                          const f4*, f4*, f4*, hipStream_t);
 size_t shade_counter_words();
 void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
 void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
@@ -88,7 +90,8 @@ struct fr_ctx {
   bool light_pending = false;
   bool compacted = false;
   bool mask_dirty = false;
-  hipEvent_t ev[10] = {};
+  hipEvent_t ev[12] = {};
+  bool time_kernels = false;  // fr_frame with timing: also time the path-trace kernel alone
   // scene export copies
   std::vector<const float*> tex_ptrs;
   std::vector<int32_t> tex_dims, mat_pairs;
@@ -522,9 +525,13 @@ static int enqueue_shading(fr_ctx* c) {
   }
   launch_carry_history(c->U, c->mask, c->img[P_WEIGHT], c->img[c->hist_cache], c->img[c->hist_cur],
                        c->img[P_SHADING], c->stream);
-  launch_shade(c->dsc, c->U, c->active, c->ray_count, (uint32_t)((size_t)c->W * c->H), c->img[P_WEIGHT],
-               c->img[c->hist_cache], c->img[c->hist_cur], c->img[P_SHADING], c->shade_ctr, c->samples, c->stats,
-               c->stream);
+  const uint32_t N = (uint32_t)((size_t)c->W * c->H);
+  if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
+  launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache],
+                     c->shade_ctr, c->samples, c->stats, c->stream);
+  if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
+  launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache], c->samples,
+                       c->img[c->hist_cur], c->img[P_SHADING], c->stream);
   int rc = check_launch(c);
   // swapBuffer("history_cache", "history_buffer"); swapBuffer("depth_cache", "depth_buffer") (:226-227)
   std::swap(c->hist_cur, c->hist_cache);
@@ -631,7 +638,10 @@ int fr_frame(fr_ctx* c, fr_frame_timing* t) {
   if (t) hipEventRecord(ev[2], c->stream);
   if ((rc = enqueue_optimize(c))) return rc;
   if (t) hipEventRecord(ev[3], c->stream);
-  if ((rc = enqueue_shading(c))) return rc;
+  c->time_kernels = t != nullptr;
+  rc = enqueue_shading(c);
+  c->time_kernels = false;
+  if (rc) return rc;
   if (t) hipEventRecord(ev[4], c->stream);
   if ((rc = enqueue_jfa(c, FR_BUF_SHADING))) return rc;
   if (t) hipEventRecord(ev[5], c->stream);
@@ -653,6 +663,7 @@ int fr_frame(fr_ctx* c, fr_frame_timing* t) {
     t->pullpush_ms = elapsed(ev[6], ev[7]);
     t->atrous_ms = elapsed(ev[7], ev[8]);
     t->total_ms = elapsed(ev[0], ev[8]);
+    t->shade_paths_ms = elapsed(ev[9], ev[10]);
     hipMemcpy(&t->ray_count, c->ray_count, 4, hipMemcpyDeviceToHost);
   }
   return FR_OK;

@@ -78,7 +78,7 @@ class fr_stats(C.Structure):
 class fr_frame_timing(C.Structure):
     _fields_ = [(n, C.c_float) for n in ("geometry_ms", "sampling_ms", "optimize_ms", "shading_ms", "jfa_ms",
                                          "sibson_ms", "pullpush_ms", "atrous_ms", "total_ms")] + \
-               [("ray_count", C.c_uint32)]
+               [("ray_count", C.c_uint32), ("shade_paths_ms", C.c_float)]
 
 
 class fr_scene_arrays(C.Structure):

@@ -142,6 +142,7 @@ typedef struct fr_frame_timing {
   float jfa_ms, sibson_ms, pullpush_ms, atrous_ms;
   float total_ms;
   uint32_t ray_count;
+  float shade_paths_ms; /* the path-trace megakernel alone (inside shading_ms) */
 } fr_frame_timing;
 
 typedef struct fr_ctx fr_ctx;
