@@ -20,7 +20,7 @@
 namespace fr {
 void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
 void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
-                        const f4*, uint32_t*, f4*, DevStats*, hipStream_t);
+                        const f4*, uint32_t*, f4*, DevStats*, int, hipStream_t);
 void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
                           const f4*, f4*, f4*, hipStream_t);
 size_t shade_counter_words();
@@ -91,7 +91,8 @@ struct fr_ctx {
   bool compacted = false;
   bool mask_dirty = false;
   hipEvent_t ev[12] = {};
-  bool time_kernels = false;  // fr_frame with timing: also time the path-trace kernel alone
+  bool time_kernels = false;
+  int wait_threshold = 64;  // lanes (of 64) waiting before a wave leaves its traversal steps to shade (64: all)  // fr_frame with timing: also time the path-trace kernel alone
   // scene export copies
   std::vector<const float*> tex_ptrs;
   std::vector<int32_t> tex_dims, mat_pairs;
@@ -329,6 +330,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
 
   fr_ctx* c = new fr_ctx();
   c->cfg = cfg;
+  if (const char* w = getenv("FOVRT_WAIT_THRESHOLD")) c->wait_threshold = std::max(1, std::min(64, atoi(w)));
   c->asset_dir = cfg.asset_dir ? cfg.asset_dir : "assets";
   c->cfg.asset_dir = nullptr;
   c->W = cfg.width; c->H = cfg.height;
@@ -343,6 +345,10 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     return bail(FR_E_IO);
   }
   build_bvh(c->scene, c->bvh);
+  if (c->bvh.max_stack > FR_BVH_STACK) {
+    c->err = "BVH needs a traversal stack deeper than FR_BVH_STACK";
+    return bail(FR_E_UNSUPPORTED);
+  }
   const HostScene& s = c->scene;
   const int nt = s.num_tris();
   std::vector<TriShade> shade(nt);
@@ -528,7 +534,7 @@ static int enqueue_shading(fr_ctx* c) {
   const uint32_t N = (uint32_t)((size_t)c->W * c->H);
   if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
   launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache],
-                     c->shade_ctr, c->samples, c->stats, c->stream);
+                     c->shade_ctr, c->samples, c->stats, c->wait_threshold, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache], c->samples,
                        c->img[c->hist_cur], c->img[P_SHADING], c->stream);
@@ -744,6 +750,7 @@ int fr_get_stats(fr_ctx* c, fr_stats* s) {
   s->gbuffer_primary = d.gbuffer_primary; s->primary = d.primary; s->shadow = d.shadow;
   s->diffuse_bounce = d.diffuse_bounce; s->mirror = d.mirror; s->refraction = d.refraction;
   s->reflection = d.reflection; s->truncated = d.truncated; s->overflow = d.bvh_overflow;
+  for (int i = 0; i < 4; i++) s->diag[i] = d.pad[i];
   s->segments = d.gbuffer_primary + d.primary + d.shadow + d.diffuse_bounce + d.mirror + d.refraction + d.reflection;
   return FR_OK;
 }
@@ -785,6 +792,7 @@ static void fill_arrays(const HostScene& s, const Bvh& bvh, f3 emission, std::ve
   o->bbox[3] = s.bbox_max.x; o->bbox[4] = s.bbox_max.y; o->bbox[5] = s.bbox_max.z;
   o->bvh_nodes = (int)bvh.nodes.size();
   o->bvh_depth = bvh.max_depth;
+  o->bvh_max_stack = bvh.max_stack;
 }
 
 extern "C" {

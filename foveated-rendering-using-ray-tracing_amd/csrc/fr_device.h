@@ -6,20 +6,22 @@
 
 namespace fr {
 
+#define FR_BVH_STACK 32  // per-lane traversal stack entries (LDS)
+
 enum MaterialType : int32_t { MATL_DIFFUSE = 0, MATL_REFLECTION = 1, MATL_REFRACTION = 2 };
 
-// Two-wide BVH node holding BOTH children's boxes (one 64-B line per node visit).
+// Four-wide BVH node: the boxes of all four children, SoA by axis (two 64-byte lines per visit).
 // child[k] >= 0 with count[k] == 0  -> inner node index
 // count[k] > 0                      -> leaf: triangles [child[k], child[k]+count[k]) of tri_geo
-// count[k] < 0                      -> empty slot (never hit)
+// count[k] < 0                      -> empty slot (box lo = +inf, hi = -inf; never hit)
 struct alignas(16) BvhNode {
-  f4 bx;  // (c0.lo.x, c0.hi.x, c1.lo.x, c1.hi.x)
-  f4 by;  // (c0.lo.y, c0.hi.y, c1.lo.y, c1.hi.y)
-  f4 bz;  // (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
-  int32_t child[2];
-  int32_t count[2];
+  f4 lox, hix;  // child k's x slab in component k
+  f4 loy, hiy;
+  f4 loz, hiz;
+  int32_t child[4];
+  int32_t count[4];
 };
-static_assert(sizeof(BvhNode) == 64, "BvhNode must be one 64-byte line");
+static_assert(sizeof(BvhNode) == 128, "BvhNode must be two 64-byte lines");
 
 // Leaf-ordered triangle, pre-differenced exactly as optix::intersect_triangle does at run time
 // (e0 = p1 - p0, e1 = p0 - p2, n = cross(e1, e0); optixu_math_namespace.h, PTX

@@ -613,31 +613,77 @@ struct Builder {
     }
     return mid;
   }
-  void set_box(BvhNode& nd, int k, const Box& bx) {
-    float* X = &nd.bx.x; float* Y = &nd.by.x; float* Z = &nd.bz.x;
-    X[2 * k] = inflate_lo(bx.lo.x); X[2 * k + 1] = inflate_hi(bx.hi.x);
-    Y[2 * k] = inflate_lo(bx.lo.y); Y[2 * k + 1] = inflate_hi(bx.hi.y);
-    Z[2 * k] = inflate_lo(bx.lo.z); Z[2 * k + 1] = inflate_hi(bx.hi.z);
+  // Binary build: node i has children (box2[2i+k], child2[2i+k], count2[2i+k]), k = 0, 1.
+  std::vector<Box> box2;
+  std::vector<int32_t> child2, count2;
+  int new_node2() {
+    box2.resize(box2.size() + 2); child2.resize(child2.size() + 2); count2.resize(count2.size() + 2);
+    return (int)child2.size() / 2 - 1;
   }
-  // Builds node `ni` whose two children are [b,mid) and [mid,e).
   void build_node(int ni, int b, int mid, int e, int depth) {
-    out.max_depth = std::max(out.max_depth, depth);
     int ranges[2][2] = {{b, mid}, {mid, e}};
     for (int k = 0; k < 2; k++) {
       int cb = ranges[k][0], ce = ranges[k][1];
-      Box bx = range_box(cb, ce);
-      set_box(out.nodes[ni], k, bx);
+      box2[2 * ni + k] = range_box(cb, ce);
       int sp = split(cb, ce, depth + 1);
       if (sp < 0) {
         int32_t c, cnt;
         emit_leaf(cb, ce, c, cnt);
-        out.nodes[ni].child[k] = c; out.nodes[ni].count[k] = cnt;
+        child2[2 * ni + k] = c; count2[2 * ni + k] = cnt;
       } else {
-        int child = (int)out.nodes.size();
-        out.nodes.push_back(BvhNode{});
-        out.nodes[ni].child[k] = child; out.nodes[ni].count[k] = 0;
+        int child = new_node2();
+        child2[2 * ni + k] = child; count2[2 * ni + k] = 0;
         build_node(child, cb, sp, ce, depth + 1);
       }
+    }
+  }
+  // Collapse into four-wide nodes: repeatedly open the largest-area inner entry until four entries.
+  // The inner children of a node are stored contiguously, so one traversal stack entry (the base
+  // index + the near-to-far order of the remaining children) covers a whole level.
+  struct Entry { Box box; int32_t child, count; };
+  void collapse(const std::vector<Entry>& seed, int ni, int depth, int stack_need) {
+    std::vector<Entry> ents = seed;
+    while (ents.size() < 4) {
+      int best = -1; float ba = -1.0f;
+      for (size_t i = 0; i < ents.size(); i++)
+        if (ents[i].count == 0 && ents[i].box.area() > ba) { ba = ents[i].box.area(); best = (int)i; }
+      if (best < 0) break;
+      int n2 = ents[best].child;
+      ents.erase(ents.begin() + best);
+      for (int k = 0; k < 2; k++) ents.push_back(Entry{box2[2 * n2 + k], child2[2 * n2 + k], count2[2 * n2 + k]});
+    }
+    out.max_depth = std::max(out.max_depth, depth);
+    int inner = 0;
+    for (auto& e : ents) inner += e.count == 0;
+    const int need = stack_need + (inner > 1 ? 1 : 0);
+    out.max_stack = std::max(out.max_stack, need);
+    const int base = (int)out.nodes.size();
+    out.nodes.resize(out.nodes.size() + inner);
+    BvhNode& nd = out.nodes[ni];
+    float* LX = &nd.lox.x; float* HX = &nd.hix.x;
+    float* LY = &nd.loy.x; float* HY = &nd.hiy.x;
+    float* LZ = &nd.loz.x; float* HZ = &nd.hiz.x;
+    int r = 0;
+    for (int k = 0; k < 4; k++) {
+      if (k >= (int)ents.size()) {
+        LX[k] = LY[k] = LZ[k] = INFINITY; HX[k] = HY[k] = HZ[k] = -INFINITY;
+        nd.child[k] = 0; nd.count[k] = -1;
+        continue;
+      }
+      const Box& bx = ents[k].box;
+      LX[k] = inflate_lo(bx.lo.x); HX[k] = inflate_hi(bx.hi.x);
+      LY[k] = inflate_lo(bx.lo.y); HY[k] = inflate_hi(bx.hi.y);
+      LZ[k] = inflate_lo(bx.lo.z); HZ[k] = inflate_hi(bx.hi.z);
+      nd.count[k] = ents[k].count;
+      nd.child[k] = ents[k].count == 0 ? base + r++ : ents[k].child;
+    }
+    r = 0;
+    for (int k = 0; k < (int)ents.size(); k++) {
+      if (ents[k].count != 0) continue;
+      int n2 = ents[k].child;
+      std::vector<Entry> sub = {Entry{box2[2 * n2], child2[2 * n2], count2[2 * n2]},
+                                Entry{box2[2 * n2 + 1], child2[2 * n2 + 1], count2[2 * n2 + 1]}};
+      collapse(sub, base + r++, depth + 1, need);
     }
   }
   void run() {
@@ -649,22 +695,21 @@ struct Builder {
       cen[i] = (b.lo + b.hi) * 0.5f;
       ids[i] = i;
     }
-    out.nodes.clear(); out.tri_prim.clear(); out.max_depth = 0; out.root_count = 0;
-    out.nodes.push_back(BvhNode{});
+    out.nodes.clear(); out.tri_prim.clear(); out.max_depth = 0; out.max_stack = 0; out.root_count = 0;
+    box2.clear(); child2.clear(); count2.clear();
     int sp = split(0, n, 0);
-    if (sp < 0) {  // tiny scene: children = [0,n) leaf and an empty slot
-      Box bx = range_box(0, n);
-      set_box(out.nodes[0], 0, bx);
+    std::vector<Entry> root;
+    if (sp < 0) {  // tiny scene: the root holds one leaf
       int32_t c, cnt; emit_leaf(0, n, c, cnt);
-      out.nodes[0].child[0] = c; out.nodes[0].count[0] = cnt;
-      set_box(out.nodes[0], 1, Box{});
-      out.nodes[0].bx.z = INFINITY; out.nodes[0].bx.w = -INFINITY;
-      out.nodes[0].by.z = INFINITY; out.nodes[0].by.w = -INFINITY;
-      out.nodes[0].bz.z = INFINITY; out.nodes[0].bz.w = -INFINITY;
-      out.nodes[0].child[1] = 0; out.nodes[0].count[1] = -1;
+      root.push_back(Entry{range_box(0, n), c, cnt});
     } else {
-      build_node(0, 0, sp, n, 0);
+      int r = new_node2();
+      build_node(r, 0, sp, n, 0);
+      root.push_back(Entry{box2[0], child2[0], count2[0]});
+      root.push_back(Entry{box2[1], child2[1], count2[1]});
     }
+    out.nodes.resize(1);
+    collapse(root, 0, 0, 0);
     out.tri_geo.resize(out.tri_prim.size());
     for (size_t i = 0; i < out.tri_prim.size(); i++) {
       int p = out.tri_prim[i];

@@ -39,6 +39,7 @@ struct Bvh {
   std::vector<int32_t> tri_prim;  // leaf order -> primitive
   int root_count = 0;             // >0 when the root itself is a leaf
   int max_depth = 0;
+  int max_stack = 0;              // deepest traversal stack any root-to-leaf path can need
 };
 
 enum ScenePreset { PRESET_BOX = 0, PRESET_BUNNY = 1, PRESET_VOKSELIA = 2 };
@@ -52,7 +53,8 @@ bool load_ppm(const std::string& path, HostTexture& tex, std::string& err);
 bool load_hdr(const std::string& path, HostTexture& tex, std::string& err);
 bool load_png(const std::string& path, HostTexture& tex, std::string& err);
 
-// Binned-SAH BVH over the soup; conservative (inflated) child boxes, depth <= 31.
+// Binned-SAH binary BVH over the soup collapsed into four-wide nodes; conservative (inflated)
+// child boxes.
 void build_bvh(const HostScene& s, Bvh& out);
 
 // Camera presets (FR/main.cpp:189-209): eye and look-at target.

@@ -134,6 +134,7 @@ typedef struct fr_stats {
   uint64_t truncated;         /* refraction nodes cut by refraction_max_depth */
   uint64_t overflow;          /* work items dropped (explicit stack full) */
   uint64_t segments;          /* sum of all traced ray segments */
+  uint64_t diag[4];           /* cycle stamps of a diagnostic build (-DFR_STAMPS), else 0 */
 } fr_stats;
 
 typedef struct fr_frame_timing {
@@ -213,7 +214,8 @@ typedef struct fr_scene_arrays {
   int envmap;
   float light[15];       /* position, v1, v2, normal, emission */
   float bbox[6];         /* min, max */
-  int bvh_nodes, bvh_depth;
+  int bvh_nodes, bvh_depth;  /* four-wide nodes, levels */
+  int bvh_max_stack;        /* deepest traversal stack the tree can need (<= 32) */
 } fr_scene_arrays;
 int fr_scene_export(fr_ctx* ctx, fr_scene_arrays* out);
 
