@@ -91,8 +91,8 @@ struct fr_ctx {
   bool compacted = false;
   bool mask_dirty = false;
   hipEvent_t ev[12] = {};
-  bool time_kernels = false;
-  int wait_threshold = 64;  // lanes (of 64) waiting before a wave leaves its traversal steps to shade (64: all)  // fr_frame with timing: also time the path-trace kernel alone
+  bool time_kernels = false;  // fr_frame with timing: also time the path-trace kernel alone
+  int wait_threshold = 64;    // lanes (of 64) waiting before a wave leaves its traversal steps to shade (64: all)
   // scene export copies
   std::vector<const float*> tex_ptrs;
   std::vector<int32_t> tex_dims, mat_pairs;

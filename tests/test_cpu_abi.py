@@ -171,3 +171,18 @@ def test_texture_loaders_match_numpy(fovrt_mod):
     found = {t.shape[:2]: t for t in tex}
     assert np.array_equal(found[(64, 64)][..., :3], grid)
     assert np.array_equal(found[(1024, 1024)][..., :3], bunny)
+
+
+def test_cpp_facade_driver_builds_and_fails_cleanly_without_gpu():
+    """include/fovrt.hpp compiles with a plain host compiler (no HIP headers) and the driver reports a
+    missing device through the facade instead of crashing."""
+    import os
+    import subprocess
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "foveated-rendering-using-ray-tracing_amd")
+    subprocess.run(["make", "-s", "-C", pkg, "fovrt_run"], check=True, timeout=300)
+    r = subprocess.run([os.path.join(pkg, "fovrt_run"), "32", "32", "--frames", "1"], capture_output=True,
+                       text=True, timeout=60)
+    import torch
+    if not torch.cuda.is_available():
+        assert r.returncode == 1 and "initialize failed" in r.stderr

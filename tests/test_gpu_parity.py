@@ -250,3 +250,36 @@ def test_full_size_frame_properties(fovrt_mod):
     assert st["overflow"] == 0
     assert st["primary"] == 2 * n * 4
     assert st["gbuffer_primary"] == 2 * W * H
+
+
+# ---------------------------------------------------------------------------------------------
+# The C++ facades (include/fovrt.hpp): the headless main.cpp-shaped driver gives the same images
+# as the Python mirror driving the same C ABI calls
+# ---------------------------------------------------------------------------------------------
+def test_cpp_facade_driver_matches_python(fovrt_mod, tmp_path):
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(fovrt_mod.LIB_PATH), "fovrt_run")
+    assert os.path.exists(exe), "build with make -C foveated-rendering-using-ray-tracing_amd"
+    W, H, frames = 96, 64, 2
+    out = tmp_path / "atrous.pfm"
+    args = [exe, str(W), str(H), "--scene", "bunny", "--mask", "logpolar10", "--spp", "4", "--dmd", "3",
+            "--frames", str(frames), "--dump", "ATROUS", str(out), "--assets", ASSET_DIR]
+    if TEXTURE_MODE == 1:
+        args.append("--procedural")
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.count("ray count") == frames
+    with open(out, "rb") as f:
+        assert f.readline().strip() == b"PF"
+        w, h = map(int, f.readline().split())
+        assert (w, h) == (W, H) and float(f.readline()) < 0
+        img = np.frombuffer(f.read(), dtype="<f4").reshape(H, W, 3)
+    t = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    for _ in range(frames):
+        t.geometry_launch(); t.sampling_launch(); t.optimize_launch(); t.shading_launch()
+        fovrt_mod.JumpFlooding(t).render(TN.SHADING)
+        fovrt_mod.SibsonInterpolation(t).render()
+        fovrt_mod.PullPushInterpolation(t).render(TN.SHADING)
+        fovrt_mod.ATrous(t).render(1, TN.POSITION, TN.NORMAL, TN.PULLPUSH)
+    assert equal_nan(img, t.read(TN.ATROUS)[..., :3])
