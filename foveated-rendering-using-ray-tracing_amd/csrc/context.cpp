@@ -31,7 +31,7 @@ void launch_mask_words(const uint8_t*, const uint8_t*, int, int, unsigned long l
 void launch_compaction(int, int, const unsigned long long*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                        uint32_t*, hipStream_t);
 size_t compaction_tiles(int W, int H);
-void launch_jfa(const f4*, uint32_t*, uint32_t*, float*, float*, f4*, f4*, int, int, hipStream_t);
+void launch_jfa(const f4*, u2*, u2*, f4*, f4*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
 void launch_pullpush(const f4*, f4*, f4*, f4*, f4*, int, int, hipStream_t);
 void launch_atrous(const f4*, const f4*, const f4*, f4*, int, int, float, float, float, float, hipStream_t);
@@ -80,8 +80,7 @@ struct fr_ctx {
   uint32_t* active = nullptr;
   uint32_t* shade_ctr = nullptr;  // sharded chunk counters of the shading work queue
   f4* samples = nullptr;          // one radiance value per (active pixel, camera sample)
-  uint32_t *jfa_a = nullptr, *jfa_b = nullptr;
-  float *jfa_colx = nullptr, *jfa_coly = nullptr;
+  u2 *jfa_a = nullptr, *jfa_b = nullptr;  // JFA state ping-pong (seed coord texel + alpha flags)
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
   int pp_S = 0;
   DevStats* stats = nullptr;
@@ -401,7 +400,6 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       dalloc(&c->counts, 4 * nblocks) != hipSuccess || dalloc(&c->offsets, 4 * nblocks) != hipSuccess ||
       dalloc(&c->tiles, 1024) != hipSuccess || dalloc(&c->ray_count, 4) != hipSuccess ||
       dalloc(&c->active, N) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
-      dalloc(&c->jfa_colx, (size_t)c->W) != hipSuccess || dalloc(&c->jfa_coly, (size_t)c->H) != hipSuccess ||
       dalloc(&c->pull, atlas) != hipSuccess || dalloc(&c->push, atlas) != hipSuccess ||
       dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess ||
       dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, N * cfg.spp) != hipSuccess) {
@@ -446,7 +444,7 @@ int fr_destroy(fr_ctx* c) {
   for (auto p : c->d_tex) fr(p);
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
-  fr(c->mask); fr(c->gclass); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->jfa_a); fr(c->jfa_b); fr(c->jfa_colx); fr(c->jfa_coly);
+  fr(c->mask); fr(c->gclass); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->jfa_a); fr(c->jfa_b);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -569,7 +567,7 @@ static int resolve(fr_ctx* c, int id, int* phys) {
 static int enqueue_jfa(fr_ctx* c, int in_buffer) {
   int p;
   if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "jfa: bad input buffer");
-  launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->jfa_colx, c->jfa_coly, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->W, c->H, c->stream);
+  launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->W, c->H, c->stream);
   return check_launch(c);
 }
 static int enqueue_sibson(fr_ctx* c) {
