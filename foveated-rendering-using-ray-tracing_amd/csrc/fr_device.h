@@ -6,7 +6,7 @@
 
 namespace fr {
 
-#define FR_BVH_STACK 32  // per-lane traversal stack entries (LDS)
+#define FR_BVH_STACK 24  // per-lane traversal stack entries (LDS; one per BVH level)
 
 enum MaterialType : int32_t { MATL_DIFFUSE = 0, MATL_REFLECTION = 1, MATL_REFRACTION = 2 };
 

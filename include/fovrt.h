@@ -215,7 +215,7 @@ typedef struct fr_scene_arrays {
   float light[15];       /* position, v1, v2, normal, emission */
   float bbox[6];         /* min, max */
   int bvh_nodes, bvh_depth;  /* four-wide nodes, levels */
-  int bvh_max_stack;        /* deepest traversal stack the tree can need (<= 32) */
+  int bvh_max_stack;        /* deepest traversal stack the tree can need (<= 24) */
 } fr_scene_arrays;
 int fr_scene_export(fr_ctx* ctx, fr_scene_arrays* out);
 

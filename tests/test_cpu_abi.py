@@ -122,7 +122,7 @@ def test_scene_presets(fovrt_mod, scene, ntri_min):
     vn = a["nrm"].reshape(-1, 3, 3).sum(1)
     agree = (np.einsum("ij,ij->i", n[has_n], vn[has_n]) > 0).mean()
     assert agree > 0.99
-    assert a["bvh_depth"] <= 31 and 0 <= a["bvh_max_stack"] <= 32
+    assert a["bvh_depth"] <= 31 and 0 <= a["bvh_max_stack"] <= 24
 
 
 def read_ppm_np(path):
