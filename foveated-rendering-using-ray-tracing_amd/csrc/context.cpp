@@ -31,6 +31,8 @@ void launch_mask_words(const uint8_t*, const uint8_t*, int, int, unsigned long l
 void launch_compaction(int, int, const unsigned long long*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                        uint32_t*, hipStream_t);
 size_t compaction_tiles(int W, int H);
+void launch_shard_pack(const FrameUniforms&, const f4*, f4*, hipStream_t);
+void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
 void launch_pullpush(const f4*, f4*, f4*, f4*, f4*, int, int, hipStream_t);
@@ -417,6 +419,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   U.spp = cfg.spp;
   U.sqrt_spp = (int)floor(sqrt((double)cfg.spp) + 1e-9);
   U.mask_mode = cfg.mask_mode;
+  U.shard_rank = 0; U.shard_count = 1; U.shard_tile = 128; U.shard_tiles_x = (c->W + 127) / 128;
   {
     fr_camera_pose pose;
     float eye[3], tgt[3], upv[3] = {0, 1, 0};
@@ -630,30 +633,43 @@ int fr_atrous_render(fr_ctx* c, int count, int pos, int nrm, int col, uint64_t* 
   return ns_timed(c, [&] { return enqueue_atrous(c, count, pos, nrm, col); }, ns);
 }
 
-int fr_frame(fr_ctx* c, fr_frame_timing* t) {
+// Frame halves: the trace half (update -> entries 0..3) and the reconstruction half (JFA -> SI ->
+// PPI -> AT). fr_frame runs both; a tile-sharded view runs the trace half on every rank and the
+// reconstruction half on the rank that composites (after fr_shard_unpack of the other ranks' tiles).
+static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
   if (!c) return FR_E_INVALID;
   hipSetDevice(c->cfg.device);
   hipEvent_t* ev = c->ev;
-  if (t) hipEventRecord(ev[0], c->stream);
   int rc;
-  if ((rc = enqueue_geometry(c))) return rc;
-  if (t) hipEventRecord(ev[1], c->stream);
-  if ((rc = enqueue_sampling(c))) return rc;
-  if (t) hipEventRecord(ev[2], c->stream);
-  if ((rc = enqueue_optimize(c))) return rc;
-  if (t) hipEventRecord(ev[3], c->stream);
-  c->time_kernels = t != nullptr;
-  rc = enqueue_shading(c);
-  c->time_kernels = false;
-  if (rc) return rc;
+  if (t) hipEventRecord(ev[0], c->stream);
+  if (trace) {
+    if ((rc = enqueue_geometry(c))) return rc;
+    if (t) hipEventRecord(ev[1], c->stream);
+    if ((rc = enqueue_sampling(c))) return rc;
+    if (t) hipEventRecord(ev[2], c->stream);
+    if ((rc = enqueue_optimize(c))) return rc;
+    if (t) hipEventRecord(ev[3], c->stream);
+    c->time_kernels = t != nullptr;
+    rc = enqueue_shading(c);
+    c->time_kernels = false;
+    if (rc) return rc;
+  } else if (t) {
+    for (int i = 1; i <= 3; i++) hipEventRecord(ev[i], c->stream);
+    hipEventRecord(ev[9], c->stream);
+    hipEventRecord(ev[10], c->stream);
+  }
   if (t) hipEventRecord(ev[4], c->stream);
-  if ((rc = enqueue_jfa(c, FR_BUF_SHADING))) return rc;
-  if (t) hipEventRecord(ev[5], c->stream);
-  if ((rc = enqueue_sibson(c))) return rc;
-  if (t) hipEventRecord(ev[6], c->stream);
-  if ((rc = enqueue_pullpush(c, FR_BUF_SHADING))) return rc;
-  if (t) hipEventRecord(ev[7], c->stream);
-  if ((rc = enqueue_atrous(c, c->cfg.atrous_iterations, FR_BUF_POSITION, FR_BUF_NORMAL, FR_BUF_PULLPUSH))) return rc;
+  if (recon) {
+    if ((rc = enqueue_jfa(c, FR_BUF_SHADING))) return rc;
+    if (t) hipEventRecord(ev[5], c->stream);
+    if ((rc = enqueue_sibson(c))) return rc;
+    if (t) hipEventRecord(ev[6], c->stream);
+    if ((rc = enqueue_pullpush(c, FR_BUF_SHADING))) return rc;
+    if (t) hipEventRecord(ev[7], c->stream);
+    if ((rc = enqueue_atrous(c, c->cfg.atrous_iterations, FR_BUF_POSITION, FR_BUF_NORMAL, FR_BUF_PULLPUSH))) return rc;
+  } else if (t) {
+    for (int i = 5; i <= 7; i++) hipEventRecord(ev[i], c->stream);
+  }
   if (t) {
     hipEventRecord(ev[8], c->stream);
     hipError_t e = hipEventSynchronize(ev[8]);
@@ -671,6 +687,55 @@ int fr_frame(fr_ctx* c, fr_frame_timing* t) {
     hipMemcpy(&t->ray_count, c->ray_count, 4, hipMemcpyDeviceToHost);
   }
   return FR_OK;
+}
+
+int fr_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, true, true); }
+int fr_trace_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, true, false); }
+int fr_reconstruct_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, false, true); }
+
+int fr_set_shard(fr_ctx* c, int rank, int count, int tile) {
+  if (!c) return FR_E_INVALID;
+  if (count < 1 || rank < 0 || rank >= count || tile < 8 || tile > 4096)
+    return fail(c, FR_E_INVALID, "fr_set_shard: need 0 <= rank < count and 8 <= tile <= 4096");
+  c->U.shard_rank = rank;
+  c->U.shard_count = count;
+  c->U.shard_tile = tile;
+  c->U.shard_tiles_x = (c->W + tile - 1) / tile;
+  c->compacted = false;
+  return FR_OK;
+}
+
+int fr_shard_texels(fr_ctx* c, size_t* texels) {
+  if (!c || !texels) return FR_E_INVALID;
+  const int T = c->U.shard_count > 1 ? c->U.shard_tile : 0;
+  if (!T) { *texels = (size_t)c->W * c->H; return FR_OK; }
+  const size_t tiles = (size_t)c->U.shard_tiles_x * ((c->H + T - 1) / T);
+  *texels = (tiles + c->U.shard_count - 1) / c->U.shard_count * (size_t)T * T;
+  return FR_OK;
+}
+
+static int shard_io(fr_ctx* c, int id, int rank, void* slab, size_t bytes, bool pack) {
+  if (!c || !slab) return FR_E_INVALID;
+  if (c->U.shard_count <= 1) return fail(c, FR_E_STATE, "fr_shard_*: call fr_set_shard with count > 1 first");
+  if (rank < 0 || rank >= c->U.shard_count) return fail(c, FR_E_INVALID, "fr_shard_unpack: bad source rank");
+  int p;
+  if (resolve(c, id, &p)) return fail(c, FR_E_INVALID, "fr_shard_*: buffer is not an RGBA32F image");
+  size_t texels = 0;
+  fr_shard_texels(c, &texels);
+  if (bytes < texels * sizeof(f4)) return fail(c, FR_E_INVALID, "fr_shard_*: slab smaller than fr_shard_texels * 16");
+  hipSetDevice(c->cfg.device);
+  if (pack) launch_shard_pack(c->U, c->img[p], (f4*)slab, c->stream);
+  else launch_shard_unpack(c->U, rank, (const f4*)slab, c->img[p], c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FR_OK;
+}
+int fr_shard_pack(fr_ctx* c, int id, void* slab, size_t bytes) {
+  return shard_io(c, id, c ? c->U.shard_rank : 0, slab, bytes, true);
+}
+int fr_shard_unpack(fr_ctx* c, int id, int src_rank, const void* slab, size_t bytes) {
+  return shard_io(c, id, src_rank, const_cast<void*>(slab), bytes, false);
 }
 
 int fr_synchronize(fr_ctx* c) {

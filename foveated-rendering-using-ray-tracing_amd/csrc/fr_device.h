@@ -88,7 +88,16 @@ struct FrameUniforms {
   int32_t spp;
   int32_t sqrt_spp;
   int32_t mask_mode;
+  // screen-tile sharding of one view across ranks (fr_set_shard): tile t = ty * tiles_x + tx is
+  // traced by rank t % shard_count; shard_count 1 = the whole screen
+  int32_t shard_rank, shard_count, shard_tile, shard_tiles_x;
 };
+
+FR_HD bool shard_owns(const FrameUniforms& U, int x, int y) {
+  if (U.shard_count <= 1) return true;
+  const int t = (y / U.shard_tile) * U.shard_tiles_x + x / U.shard_tile;
+  return t % U.shard_count == U.shard_rank;
+}
 
 // Ray-segment statistics, accumulated with one atomic per wave.
 struct DevStats {

@@ -119,6 +119,12 @@ _SIGS = {
     "fr_pullpush_render": [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)],
     "fr_atrous_render": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64)],
     "fr_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
+    "fr_trace_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
+    "fr_reconstruct_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
+    "fr_set_shard": [C.c_void_p, C.c_int, C.c_int, C.c_int],
+    "fr_shard_texels": [C.c_void_p, C.POINTER(C.c_size_t)],
+    "fr_shard_pack": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
+    "fr_shard_unpack": [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t],
     "fr_synchronize": [C.c_void_p],
     "fr_get_buffer": [C.c_void_p, C.c_int, C.POINTER(fr_buffer_view)],
     "fr_read_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
@@ -400,13 +406,42 @@ class PathTracer:
     def reset_stats(self):
         self._check(_lib.fr_reset_stats(self._ctx))
 
-    def frame(self, timing=True):
-        """One iteration of the FR/main.cpp:253-358 loop body on the device."""
+    def _frame(self, fn, timing):
         t = fr_frame_timing() if timing else None
-        self._check(_lib.fr_frame(self._ctx, C.byref(t) if timing else None))
+        self._check(fn(self._ctx, C.byref(t) if timing else None))
         if not timing:
             return None
         return {n: getattr(t, n) for n, _ in fr_frame_timing._fields_}
+
+    def frame(self, timing=True):
+        """One iteration of the FR/main.cpp:253-358 loop body on the device."""
+        return self._frame(_lib.fr_frame, timing)
+
+    def trace_frame(self, timing=True):
+        """The trace half of a frame (update -> entries 0..3)."""
+        return self._frame(_lib.fr_trace_frame, timing)
+
+    def reconstruct_frame(self, timing=True):
+        """The reconstruction half of a frame (JFA -> Sibson -> pull-push -> A-Trous)."""
+        return self._frame(_lib.fr_reconstruct_frame, timing)
+
+    # tile sharding of one view across ranks (include/fovrt.h, fr_set_shard)
+    def set_shard(self, rank, count, tile=128):
+        self._check(_lib.fr_set_shard(self._ctx, int(rank), int(count), int(tile)))
+
+    def shard_texels(self) -> int:
+        n = C.c_size_t()
+        self._check(_lib.fr_shard_texels(self._ctx, C.byref(n)))
+        return n.value
+
+    def shard_pack(self, buffer_id, device_ptr, nbytes):
+        """Packs this rank's tiles of an RGBA32F buffer into the device slab at device_ptr."""
+        self._check(_lib.fr_shard_pack(self._ctx, int(buffer_id), C.c_void_p(device_ptr), int(nbytes)))
+
+    def shard_unpack(self, buffer_id, src_rank, device_ptr, nbytes):
+        """Writes rank src_rank's tiles from the device slab at device_ptr into the buffer."""
+        self._check(_lib.fr_shard_unpack(self._ctx, int(buffer_id), int(src_rank), C.c_void_p(device_ptr),
+                                         int(nbytes)))
 
     def synchronize(self):
         self._check(_lib.fr_synchronize(self._ctx))

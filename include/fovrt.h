@@ -189,7 +189,22 @@ int fr_atrous_render(fr_ctx* ctx, int count, int pos_buffer, int nrm_buffer, int
 /* The whole main.cpp loop body (update -> 0 -> 1 -> 2 -> 3 -> JFA -> SI -> PPI -> AT), enqueued on the
  * context stream. timing may be NULL (no host synchronisation then; call fr_synchronize). */
 int fr_frame(fr_ctx* ctx, fr_frame_timing* timing);
+int fr_trace_frame(fr_ctx* ctx, fr_frame_timing* timing);        /* update -> entries 0..3 only */
+int fr_reconstruct_frame(fr_ctx* ctx, fr_frame_timing* timing);  /* JFA -> SI -> PPI -> AT only */
 int fr_synchronize(fr_ctx* ctx);
+
+/* Tile sharding of one view across ranks (BASELINE configs[3]): screen tiles of
+ * tile x tile pixels, tile t = ty * ceil(W / tile) + tx traced by rank t % count (round robin, so
+ * the dense foveal tiles spread over all ranks). Every rank computes the full G-buffer and sampling
+ * mask and traces only its own tiles' active pixels; the compositing rank unpacks the other ranks'
+ * tiles of SHADING and runs the reconstruction half. Exact for a static camera (history is
+ * per-tile); with a moving camera also exchange HISTORY_CACHE the same way. count = 1 restores the
+ * whole screen. Slabs are device buffers of fr_shard_texels() RGBA32F texels (T*T per owned tile,
+ * owned tiles in increasing order); pack/unpack synchronise the context stream. */
+int fr_set_shard(fr_ctx* ctx, int rank, int count, int tile);
+int fr_shard_texels(fr_ctx* ctx, size_t* texels);
+int fr_shard_pack(fr_ctx* ctx, int buffer_id, void* device_slab, size_t bytes);
+int fr_shard_unpack(fr_ctx* ctx, int buffer_id, int src_rank, const void* device_slab, size_t bytes);
 
 /* Buffer access (PathTracer::get_texture, FR/PathTracer.cpp:337-374; rtBufferMap). */
 int fr_get_buffer(fr_ctx* ctx, int id, fr_buffer_view* view);

@@ -283,3 +283,36 @@ def test_cpp_facade_driver_matches_python(fovrt_mod, tmp_path):
         fovrt_mod.PullPushInterpolation(t).render(TN.SHADING)
         fovrt_mod.ATrous(t).render(1, TN.POSITION, TN.NORMAL, TN.PULLPUSH)
     assert equal_nan(img, t.read(TN.ATROUS)[..., :3])
+
+
+# ---------------------------------------------------------------------------------------------
+# Tile sharding (BASELINE configs[3]): ranks trace their own screen tiles, the root
+# unpacks the others' shading tiles and reconstructs; the composite equals the one-GPU frame.
+# Rehearsed here with three contexts on one device (one process), slabs in torch device memory.
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("nranks,tile", [(2, 64), (3, 32)])
+def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile):
+    import torch
+    W, H = 200, 136  # not multiples of the tile: clipped border tiles
+    full = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    ranks = [make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3) for _ in range(nranks)]
+    for r, t in enumerate(ranks):
+        t.set_shard(r, nranks, tile)
+    n = ranks[0].shard_texels()
+    assert all(t.shard_texels() == n for t in ranks)
+    slabs = [torch.zeros(n * 4, dtype=torch.float32, device="cuda") for _ in range(nranks)]
+    root = ranks[0]
+    for _ in range(3):
+        full.frame(timing=False)
+        counts = [t.trace_frame(timing=True)["ray_count"] for t in ranks]
+        for r, t in enumerate(ranks):
+            t.shard_pack(TN.SHADING, slabs[r].data_ptr(), n * 16)
+        for r in range(1, nranks):
+            root.shard_unpack(TN.SHADING, r, slabs[r].data_ptr(), n * 16)
+        root.reconstruct_frame(timing=False)
+        assert sum(counts) == full.ray_count()
+        assert equal_nan(root.read(TN.SHADING), full.read(TN.SHADING))
+    for tid in (TN.JFA_COLOR, TN.SIBSON, TN.PULLPUSH, TN.ATROUS):
+        assert equal_nan(root.read(tid), full.read(tid)), tid
+    masks = sum(t.read(TN.MASK).astype(np.int32) for t in ranks)
+    assert np.array_equal(masks, full.read(TN.MASK))  # the ranks' masks partition the full mask
