@@ -110,6 +110,37 @@ def reduce_over_ranks(dist, device, elapsed, segs):
     return float(t.item()), float(s.item())
 
 
+def view_layout(rank, world, views):
+    """Ranks -> views: `views` views of world / views ranks each; the ranks of a view tile-shard it
+    and composite on the view's first rank. Returns (view, rank in view, ranks per view)."""
+    if views <= 0:
+        views = world
+    if world % views:
+        raise SystemExit(f"--views {views} must divide the number of ranks {world}")
+    g = world // views
+    return rank // g, rank % g, g
+
+
+def make_view_groups(dist, world, views):
+    """One process group per view (every rank creates every group, in the same order)."""
+    g = world // views
+    return [dist.new_group(list(range(v * g, (v + 1) * g))) for v in range(views)]
+
+
+def gather_slabs(dist, group, slab, gather_list, dst):
+    """RCCL gather of every rank's packed tiles to the view's compositing rank `dst` (over gloo, as
+    in the one-GPU rehearsal, device slabs are staged through host memory)."""
+    if dist.get_backend() == "gloo" and slab.is_cuda:
+        host = slab.cpu()
+        hl = [t.cpu() for t in gather_list] if gather_list is not None else None
+        dist.gather(host, gather_list=hl, dst=dst, group=group)
+        if gather_list is not None:
+            for t, h in zip(gather_list, hl):
+                t.copy_(h)
+        return
+    dist.gather(slab, gather_list=gather_list, dst=dst, group=group)
+
+
 def load_traffic(kernels, config):
     """HBM bytes per launch of `kernels` from the newest profiles/*_pmc_traffic.json recorded on the
     same workload (scripts/profile.sh), else None."""
@@ -144,6 +175,10 @@ def main():
     ap.add_argument("--refraction-max-depth", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-scale", type=int, default=1, help="CPU baseline at 1/scale resolution per axis")
+    ap.add_argument("--views", type=int, default=0,
+                    help="views rendered by the job (0: one per rank = weak scaling); the ranks of a view "
+                         "tile-shard it and gather the tiles to the view's first rank for reconstruction")
+    ap.add_argument("--tile", type=int, default=128, help="screen tile size of the tile sharding")
     args = ap.parse_args()
     args.mask = fovrt.MASKS[args.mask]
     scene = fovrt.SCENES[args.scene]
@@ -156,7 +191,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("FOVRT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local_rank)
         dist.init_process_group(backend=backend)
@@ -171,20 +206,55 @@ def main():
             dist.barrier()
 
     W, H = args.width, args.height
+    # one GPU per rank; more ranks than GPUs (the gloo rehearsal on a one-GPU box) share them
+    ndev = max(1, torch.cuda.device_count())
+    device = local_rank % ndev
+    views = args.views or world
+    view, vrank, G = view_layout(rank, world, views)
+    groups = make_view_groups(dist, world, views) if dist is not None and G > 1 else None
     cfg = fovrt.Config(width=W, height=H, scene=scene, mask_mode=args.mask, spp=args.spp, diffuse_max_depth=args.dmd,
-                       refraction_max_depth=args.refraction_max_depth, device=local_rank)
+                       refraction_max_depth=args.refraction_max_depth, device=device)
     tracer = fovrt.PathTracer(cfg)
     tracer.initialize()
     cam = fovrt.Camera.preset(scene, W, H)
-    # weak scaling: rank r renders its own view (eye offset along x, 6.4 cm per view)
-    if world > 1:
-        cam.setPosition(np.asarray(cam.pos) + view_offset(rank, world))
+    # each view is its own eye/camera (offset along x, 6.4 cm per view)
+    if views > 1:
+        cam.setPosition(np.asarray(cam.pos) + view_offset(view, views))
         cam.lookAt(cam.target)
     tracer.update_optix_variables(cam)
 
+    slab = gather_list = None
+    if G > 1:
+        tracer.set_shard(vrank, G, args.tile)
+        n_tex = tracer.shard_texels()
+        slab = torch.empty(n_tex * 4, dtype=torch.float32, device=f"cuda:{device}")
+        if vrank == 0:
+            gather_list = [torch.empty_like(slab) for _ in range(G)]
+        nbytes = n_tex * 16
+        root = view * G
+
+    def step(timing):
+        """One frame of the view: the whole chain on one rank, or trace -> pack -> gather -> (root)
+        unpack + reconstruct when the view is tile-sharded."""
+        if G == 1:
+            return tracer.frame(timing=timing)
+        tm = tracer.trace_frame(timing=timing)
+        tracer.shard_pack(fovrt.TextureName.SHADING, slab.data_ptr(), nbytes)
+        gather_slabs(dist, groups[view], slab, gather_list, root)
+        if vrank == 0:
+            sync()
+            for r in range(1, G):
+                tracer.shard_unpack(fovrt.TextureName.SHADING, r, gather_list[r].data_ptr(), nbytes)
+            rec = tracer.reconstruct_frame(timing=timing)
+            if timing:
+                for k in ("jfa_ms", "sibson_ms", "pullpush_ms", "atrous_ms"):
+                    tm[k] = rec[k]
+        return tm
+
     for _ in range(args.warmup):
-        tracer.frame(timing=False)
+        step(False)
     tracer.synchronize()
+    sync()
     tracer.reset_stats()
     stage_ms = {}
     ray_counts = []
@@ -193,7 +263,7 @@ def main():
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        tm = tracer.frame(timing=True)  # HIP events on the context stream around every stage
+        tm = step(True)  # HIP events on the context stream around every stage
         for k, v in tm.items():
             if k.endswith("_ms"):
                 stage_ms[k] = stage_ms.get(k, 0.0) + v
@@ -207,12 +277,12 @@ def main():
     segs = st["segments"]
     dev = None
     if dist is not None:
-        dev = torch.device("cuda", local_rank) if has_gpu and dist.get_backend() == "nccl" else torch.device("cpu")
+        dev = torch.device("cuda", device) if has_gpu and dist.get_backend() == "nccl" else torch.device("cpu")
     elapsed, total_segs = reduce_over_ranks(dist, dev, elapsed, segs)
 
     K = args.steps
     avg = {k[:-3]: v / K for k, v in stage_ms.items()}
-    rho = float(np.mean(ray_counts)) / (W * H)
+    rho = float(np.mean(ray_counts)) * G / (W * H)
     L = jfa_passes(W, H)
     sb = stage_bytes(W, H, rho, args.spp, L)
     stage_table = {k: {"ms": round(avg[k], 4), "GB/s": round(sb[k] / (avg[k] * 1e-3) / 1e9, 1)} for k in sb}
@@ -234,7 +304,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / K * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if G == 1 else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
@@ -242,11 +312,13 @@ def main():
                                f"log-polar mask ({'signed, ~10%' if args.mask == 4 else 'mode %d' % args.mask}), "
                                "JFA + Sibson + pull-push + A-Trous",
                    "scene": args.scene, "width": W, "height": H, "spp": args.spp, "diffuse_max_depth": args.dmd,
-                   "mask_mode": args.mask, "foveal_density": round(rho, 5), "views_per_rank": 1,
-                   "parallelism": f"views x{world} (one view per GPU)",
+                   "mask_mode": args.mask, "foveal_density": round(rho, 5), "views": views,
+                   "parallelism": (f"views x{world} (one view per GPU)" if G == 1 else
+                                   f"{views} view(s) x {G}-way {args.tile}px tile sharding, RCCL gather to the "
+                                   f"view's first rank"),
                    "procedural_meshes": "box/bunny/earth stand-ins (the reference's .obj files are absent)"},
         "fps": round(K / elapsed, 2),
-        "frames_per_s_total": round(world * K / elapsed, 2),
+        "frames_per_s_total": round(views * K / elapsed, 2),
         "rays": {k: st[k] for k in ("gbuffer_primary", "primary", "shadow", "diffuse_bounce", "mirror",
                                     "refraction", "reflection", "truncated", "overflow")},
         "stages": stage_table,

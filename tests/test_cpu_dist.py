@@ -50,3 +50,45 @@ def test_single_process_passthrough():
     import bench
     assert bench.reduce_over_ranks(None, None, 1.5, 7) == (1.5, 7.0)
     assert np.allclose(bench.view_offset(0, 1), 0)
+
+
+def _tile_worker(rank, world, views, port, q):
+    import torch
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    view, vrank, g = bench.view_layout(rank, world, views)
+    groups = bench.make_view_groups(dist, world, views)
+    slab = torch.full((8,), float(rank))
+    gl = [torch.empty_like(slab) for _ in range(g)] if vrank == 0 else None
+    bench.gather_slabs(dist, groups[view], slab, gl, view * g)
+    q.put((rank, view, vrank, g, None if gl is None else [float(t[0]) for t in gl]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tile_gather_groups_gloo_world4():
+    """4 ranks, 2 views (the stereo layout of BASELINE configs[4] at half size): each view's 2 ranks
+    gather their slabs to the view's first rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tile_worker, args=(r, 4, 2, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    out = {r: rest for r, *rest in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0] == [0, 0, 2, [0.0, 1.0]] and out[2] == [1, 0, 2, [2.0, 3.0]]
+    assert out[1][3] is None and out[3][3] is None
+
+
+def test_view_layout():
+    import bench
+    assert bench.view_layout(5, 8, 0) == (5, 0, 1)   # default: one view per rank
+    assert bench.view_layout(5, 8, 2) == (1, 1, 4)   # stereo, 4-way tiles per eye
+    assert bench.view_layout(3, 4, 1) == (0, 3, 4)   # one view tiled over 4 ranks
+    with pytest.raises(SystemExit):
+        bench.view_layout(0, 6, 4)
