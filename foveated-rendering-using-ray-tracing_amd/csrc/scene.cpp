@@ -710,6 +710,20 @@ struct Builder {
     }
     out.nodes.resize(1);
     collapse(root, 0, 0, 0);
+    // Re-lay the triangles so that the leaf children of every node are one contiguous range in slot
+    // order: a traversal step tests its node's hit leaves in a single loop.
+    {
+      std::vector<int32_t> prim;
+      prim.reserve(out.tri_prim.size());
+      for (auto& nd : out.nodes)
+        for (int k = 0; k < 4; k++)
+          if (nd.count[k] > 0) {
+            const int first = (int)prim.size();
+            for (int j = 0; j < nd.count[k]; j++) prim.push_back(out.tri_prim[nd.child[k] + j]);
+            nd.child[k] = first;
+          }
+      out.tri_prim.swap(prim);
+    }
     out.tri_geo.resize(out.tri_prim.size());
     for (size_t i = 0; i < out.tri_prim.size(); i++) {
       int p = out.tri_prim[i];
