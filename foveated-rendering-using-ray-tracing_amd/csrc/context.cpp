@@ -813,7 +813,7 @@ int fr_get_stats(fr_ctx* c, fr_stats* s) {
   s->gbuffer_primary = d.gbuffer_primary; s->primary = d.primary; s->shadow = d.shadow;
   s->diffuse_bounce = d.diffuse_bounce; s->mirror = d.mirror; s->refraction = d.refraction;
   s->reflection = d.reflection; s->truncated = d.truncated; s->overflow = d.bvh_overflow;
-  for (int i = 0; i < 4; i++) s->diag[i] = d.pad[i];
+  for (int i = 0; i < 6; i++) s->diag[i] = d.pad[i];
   s->segments = d.gbuffer_primary + d.primary + d.shadow + d.diffuse_bounce + d.mirror + d.refraction + d.reflection;
   return FR_OK;
 }

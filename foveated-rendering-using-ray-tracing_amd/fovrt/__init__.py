@@ -73,7 +73,7 @@ class fr_buffer_view(C.Structure):
 class fr_stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("gbuffer_primary", "primary", "shadow", "diffuse_bounce", "mirror",
                                           "refraction", "reflection", "truncated", "overflow", "segments")] + \
-                [("diag", C.c_uint64 * 4)]
+                [("diag", C.c_uint64 * 6)]
 
 
 class fr_frame_timing(C.Structure):

@@ -134,7 +134,8 @@ typedef struct fr_stats {
   uint64_t truncated;         /* refraction nodes cut by refraction_max_depth */
   uint64_t overflow;          /* work items dropped (explicit stack full) */
   uint64_t segments;          /* sum of all traced ray segments */
-  uint64_t diag[4];           /* cycle stamps of a diagnostic build (-DFR_STAMPS), else 0 */
+  uint64_t diag[6];           /* diagnostic build (-DFR_STAMPS) only, else 0: megakernel cycle stamps
+                                 [total, refill, shade, traversal], node visits, wave traversal steps */
 } fr_stats;
 
 typedef struct fr_frame_timing {

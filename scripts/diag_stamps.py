@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase shares of the path-trace megakernel from the -DFR_STAMPS diagnostic build
 (make -C foveated-rendering-using-ray-tracing_amd diag). Wave-level s_memtime sums:
-diag = [total, refill, path_step, traversal]. Shares only; the stamped build's run time is not a
+diag = [total, refill, shade, traversal, node visits, wave traversal steps]. Shares only; the stamped build's run time is not a
 measurement."""
 import os
 import sys
@@ -27,10 +27,13 @@ def main():
     for _ in range(5):
         tm = t.frame(timing=True)
     st = t.stats()
-    total, refill, step, trav = st["diag"]
+    total, refill, step, trav, visits, wsteps = st["diag"]
     print(f"{W}x{H} dmd {dmd}: megakernel {tm['shade_paths_ms']:.3f} ms (stamped build)")
-    print(f"  refill {refill / total:.3f}  path_step {step / total:.3f}  (traversal {trav / total:.3f}, "
-          f"shading {(step - trav) / total:.3f})  other {(total - refill - step) / total:.3f}")
+    print(f"  refill {refill / total:.3f}  traversal {trav / total:.3f}  shading {step / total:.3f}  "
+          f"other {(total - refill - step - trav) / total:.3f}")
+    segs = st["primary"] + st["shadow"] + st["diffuse_bounce"] + st["mirror"] + st["refraction"] + st["reflection"]
+    print(f"  node visits {visits / 5 / 1e6:.1f} M/frame, {visits / segs:.1f} per segment; wave traversal steps "
+          f"{wsteps / 5 / 1e6:.2f} M/frame -> lane utilisation of the traversal loop {visits / (64 * wsteps):.2f}")
     t.destroy()
 
 
