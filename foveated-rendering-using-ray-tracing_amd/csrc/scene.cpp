@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -565,8 +566,12 @@ struct Builder {
   std::vector<f3> cen;
   std::vector<int32_t> ids;
   Bvh& out;
-  static constexpr int kLeaf = 4, kBins = 16, kMaxDepth = 30;
-  Builder(const HostScene& sc, Bvh& o) : s(sc), out(o) {}
+  static constexpr int kMaxBins = 64, kMaxDepth = 30;
+  int kLeaf = 2, kBins = 16;  // leaf size and SAH bins (FOVRT_BVH_LEAF / FOVRT_BVH_BINS override, for tuning)
+  Builder(const HostScene& sc, Bvh& o) : s(sc), out(o) {
+    if (const char* v = getenv("FOVRT_BVH_LEAF")) kLeaf = std::max(1, std::min(8, atoi(v)));
+    if (const char* v = getenv("FOVRT_BVH_BINS")) kBins = std::max(2, std::min(kMaxBins, atoi(v)));
+  }
 
   Box range_box(int b, int e) const { Box bx; for (int i = b; i < e; i++) bx.grow(tb[ids[i]]); return bx; }
 
@@ -588,8 +593,8 @@ struct Builder {
     auto key = [&](int id) { f3 c = cen[id]; return axis == 0 ? c.x : axis == 1 ? c.y : c.z; };
     int mid = -1;
     if (ex > 0.0f) {
-      Box bins[kBins];
-      int cnt[kBins] = {0};
+      Box bins[kMaxBins];
+      int cnt[kMaxBins] = {0};
       auto bin_of = [&](int id) { int k = (int)((key(id) - lo) / ex * kBins); return k < 0 ? 0 : (k >= kBins ? kBins - 1 : k); };
       for (int i = b; i < e; i++) { int k = bin_of(ids[i]); cnt[k]++; bins[k].grow(tb[ids[i]]); }
       float best = INFINITY;
