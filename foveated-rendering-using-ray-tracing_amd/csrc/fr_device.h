@@ -93,6 +93,15 @@ struct FrameUniforms {
   int32_t shard_rank, shard_count, shard_tile, shard_tiles_x;
 };
 
+// XCD-aware block order: blocks b, b+8, b+16, ... share an XCD (and its L2), so hand each of the 8
+// such classes one contiguous run of tiles (row-major bands of the image) instead of every 8th tile.
+// Bijective for any block count. Returns the tile index for 2-D grid block (bx, by).
+FR_DEV uint32_t xcd_tile(uint32_t bx, uint32_t by, uint32_t gx, uint32_t gy) {
+  const uint32_t nwg = gx * gy, bid = by * gx + bx;
+  const uint32_t q = nwg / 8, r = nwg % 8, k = bid % 8, i = bid / 8;
+  return k * q + (k < r ? k : r) + i;
+}
+
 FR_HD bool shard_owns(const FrameUniforms& U, int x, int y) {
   if (U.shard_count <= 1) return true;
   const int t = (y / U.shard_tile) * U.shard_tiles_x + x / U.shard_tile;
