@@ -252,6 +252,7 @@ int fr_config_default(fr_config* c) {
   c->device = 0;
   c->texture_mode = 0;
   c->detail = 0;
+  c->mesh_mode = 0;
   c->asset_dir = nullptr;
   return FR_OK;
 }
@@ -323,6 +324,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (!(cfg.spp == 1 || cfg.spp == 2 || cfg.spp == 4 || cfg.spp == 8))
     return fail(nullptr, FR_E_UNSUPPORTED, "spp must be 1, 2, 4 or 8");
   if (cfg.mask_mode < 0 || cfg.mask_mode > 4) return fail(nullptr, FR_E_INVALID, "bad mask_mode");
+  if (cfg.mesh_mode < 0 || cfg.mesh_mode > 2) return fail(nullptr, FR_E_INVALID, "bad mesh_mode");
   if (cfg.scene < 0 || cfg.scene > 2) return fail(nullptr, FR_E_INVALID, "bad scene preset");
   if (cfg.refraction_max_depth < 0 || cfg.refraction_max_depth > 100) return fail(nullptr, FR_E_INVALID, "bad refraction_max_depth");
   int ndev = 0;
@@ -341,7 +343,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   for (auto& e : c->ev) hipEventCreate(&e);
 
   std::string err;
-  if (!build_preset_scene(cfg.scene, c->asset_dir, cfg.texture_mode, cfg.light_power, cfg.detail, c->scene, err)) {
+  if (!build_preset_scene(cfg.scene, c->asset_dir, cfg.texture_mode, cfg.light_power, cfg.detail, c->scene, err,
+                          cfg.mesh_mode)) {
     c->err = "scene: " + err;
     return bail(FR_E_IO);
   }
@@ -872,10 +875,11 @@ int fr_scene_create(const fr_config* cfg_in, fr_scene** out) {
   fr_config cfg;
   if (cfg_in) cfg = *cfg_in; else fr_config_default(&cfg);
   if (cfg.scene < 0 || cfg.scene > 2) return fail(nullptr, FR_E_INVALID, "bad scene preset");
+  if (cfg.mesh_mode < 0 || cfg.mesh_mode > 2) return fail(nullptr, FR_E_INVALID, "bad mesh_mode");
   fr_scene* sc = new fr_scene();
   std::string err;
   if (!build_preset_scene(cfg.scene, cfg.asset_dir ? cfg.asset_dir : "assets", cfg.texture_mode, cfg.light_power,
-                          cfg.detail, sc->scene, err)) {
+                          cfg.detail, sc->scene, err, cfg.mesh_mode)) {
     delete sc;
     return fail(nullptr, FR_E_IO, "scene: " + err);
   }

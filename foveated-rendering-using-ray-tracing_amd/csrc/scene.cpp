@@ -13,6 +13,8 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
+#include <tuple>
 #include <map>
 #include <sstream>
 
@@ -31,9 +33,13 @@ struct Mesh {
   bool has_n = false, has_uv = false;
 };
 
-// transform: p' = translate + scale * p (uniform scale), computed in float like optix::Matrix4x4.
+// transform: p' = translate + scale * p (uniform scale), computed in float like optix::Matrix4x4;
+// normals by the inverse transpose, n' = n / scale, not renormalised (sutil loadMesh with a
+// load_xform; shading normalises after interpolation, FR/cuda/triangle_mesh.cu:82-91).
 void bake(Mesh& m, f3 t, float s) {
   for (auto& p : m.v) p = mk3(s * p.x + t.x, s * p.y + t.y, s * p.z + t.z);
+  if (m.has_n)
+    for (auto& n : m.n) n = mk3(n.x / s, n.y / s, n.z / s);
 }
 
 void add_mesh(HostScene& sc, const Mesh& m, int material, const char* name) {
@@ -310,6 +316,75 @@ static bool read_token(std::istream& in, std::string& tok) {
   return !tok.empty();
 }
 
+// Wavefront OBJ (what sutil::loadMesh reads for the reference's models, FR/PathTracer.cpp:582-595):
+// v / vt / vn / f with v, v/vt, v//vn, v/vt/vn corners, 1-based or negative (relative) indices,
+// polygons fan-triangulated; other statements (o, g, s, usemtl, mtllib, ...) are ignored: the
+// reference binds one material program and texture per model (FR/PathTracer.cpp:676-772).
+// Normals / texcoords are kept when every face corner has them.
+static bool load_obj(const std::string& path, Mesh& m, std::string& err) {
+  std::ifstream f(path);
+  if (!f) { err = "cannot open " + path; return false; }
+  std::vector<f3> V, N;
+  std::vector<f2> T;
+  std::map<std::tuple<int, int, int>, int32_t> corner;
+  std::vector<std::tuple<int, int, int>> verts;
+  bool all_n = true, all_t = true;
+  m = Mesh();
+  std::string line;
+  int lineno = 0;
+  auto fix = [](int i, size_t n) { return i > 0 ? i - 1 : (i < 0 ? (int)n + i : -1); };
+  while (std::getline(f, line)) {
+    lineno++;
+    std::istringstream ls(line);
+    std::string tag;
+    if (!(ls >> tag) || tag[0] == '#') continue;
+    if (tag == "v") { float x, y, z; ls >> x >> y >> z; V.push_back(mk3(x, y, z)); }
+    else if (tag == "vn") { float x, y, z; ls >> x >> y >> z; N.push_back(mk3(x, y, z)); }
+    else if (tag == "vt") { float u = 0, v = 0; ls >> u >> v; T.push_back(mk2(u, v)); }
+    else if (tag == "f") {
+      std::vector<int32_t> poly;
+      std::string c;
+      while (ls >> c) {
+        int vi = 0, ti = 0, ni = 0;
+        size_t s1 = c.find('/');
+        vi = atoi(c.substr(0, s1).c_str());
+        if (s1 != std::string::npos) {
+          size_t s2 = c.find('/', s1 + 1);
+          std::string ts = c.substr(s1 + 1, s2 == std::string::npos ? std::string::npos : s2 - s1 - 1);
+          if (!ts.empty()) ti = atoi(ts.c_str());
+          if (s2 != std::string::npos) ni = atoi(c.substr(s2 + 1).c_str());
+        }
+        int a = fix(vi, V.size()), b = ti ? fix(ti, T.size()) : -1, d = ni ? fix(ni, N.size()) : -1;
+        if (a < 0 || a >= (int)V.size() || b >= (int)T.size() || d >= (int)N.size() || (ti && b < 0) || (ni && d < 0)) {
+          err = path + ":" + std::to_string(lineno) + ": face index out of range";
+          return false;
+        }
+        all_t = all_t && b >= 0;
+        all_n = all_n && d >= 0;
+        auto key = std::make_tuple(a, b, d);
+        auto it = corner.find(key);
+        if (it == corner.end()) {
+          it = corner.emplace(key, (int32_t)verts.size()).first;
+          verts.push_back(key);
+        }
+        poly.push_back(it->second);
+      }
+      for (size_t k = 1; k + 1 < poly.size(); k++) {
+        m.idx.push_back(poly[0]); m.idx.push_back(poly[k]); m.idx.push_back(poly[k + 1]);
+      }
+    }
+  }
+  m.has_n = all_n && !verts.empty();
+  m.has_uv = all_t && !verts.empty();
+  for (auto& k : verts) {
+    m.v.push_back(V[std::get<0>(k)]);
+    m.n.push_back(m.has_n ? N[std::get<2>(k)] : mk3(0.0f));
+    m.uv.push_back(m.has_uv ? T[std::get<1>(k)] : mk2(0.0f, 0.0f));
+  }
+  if (m.idx.empty()) { err = path + ": no faces"; return false; }
+  return true;
+}
+
 bool load_ppm(const std::string& path, HostTexture& tex, std::string& err) {
   std::ifstream in(path, std::ios::binary);
   if (!in) { err = "cannot open " + path; return false; }
@@ -466,7 +541,7 @@ void preset_camera(int preset, f3& eye, f3& target) {
 }
 
 bool build_preset_scene(int preset, const std::string& asset_dir, int texture_mode, float light_power, int detail,
-                        HostScene& sc, std::string& err) {
+                        HostScene& sc, std::string& err, int mesh_mode) {
   sc = HostScene();
   sc.bbox_min = mk3(INFINITY);
   sc.bbox_max = mk3(-INFINITY);
@@ -500,13 +575,22 @@ bool build_preset_scene(int preset, const std::string& asset_dir, int texture_mo
   t_white = (int)sc.texs.size();
   sc.texs.push_back(white1x1());  // earth: texture "none" -> default (1,1,1) (FR/PathTracer.cpp:593)
 
+  // The reference's meshes (FR/PathTracer.cpp:582-595) when they are present under asset_dir
+  // (mesh_mode 0) or required (2); the deterministic procedural stand-in otherwise (0) or always (1).
+  auto mesh = [&](const char* rel, Mesh& m, const std::function<Mesh()>& procedural) -> bool {
+    const std::string path = asset_dir + "/" + rel;
+    if (mesh_mode != 1 && (mesh_mode == 2 || file_exists(path))) return load_obj(path, m, err);
+    m = procedural();
+    return true;
+  };
   auto mat = [&](int type, int texid) {
     sc.mats.push_back(DevMaterial{type, texid});
     return (int)sc.mats.size() - 1;
   };
   // model 0: ground (diffuse, grid.ppm, translate(0,-0.05,0))
   {
-    Mesh g = make_ground();
+    Mesh g;
+    if (!mesh("ground.obj", g, make_ground)) return false;
     bake(g, mk3(0.0f, -0.05f, 0.0f), 1.0f);
     add_mesh(sc, g, mat(MATL_DIFFUSE, t_grid), "ground");
   }
@@ -515,12 +599,14 @@ bool build_preset_scene(int preset, const std::string& asset_dir, int texture_mo
     if (texture_mode == 1) { t_vox = (int)sc.texs.size(); sc.texs.push_back(procedural_texture(256, 256, 7)); }
     else if (!tex("vokselia_spawn/vokselia_spawn.png", 0, 0, 0, t_vox)) return false;
     int G = detail > 0 ? 96 * detail : 320;
-    Mesh v = make_voxels(G, 0.125f);
+    Mesh v;
+    if (!mesh("vokselia_spawn/vokselia_spawn.obj", v, [&] { return make_voxels(G, 0.125f); })) return false;
     add_mesh(sc, v, mat(MATL_DIFFUSE, t_vox), "vokselia_spawn");
   }
   // model 2: box (refraction, grid.ppm per the code, translate(-3.5,0.2,1.2)*scale(0.01))
   {
-    Mesh b = make_cube();
+    Mesh b;
+    if (!mesh("box/box.obj", b, make_cube)) return false;
     bake(b, mk3(-3.5f, 0.2f, 1.2f), 0.01f);
     add_mesh(sc, b, mat(MATL_REFRACTION, t_grid), "box");
   }
@@ -528,11 +614,13 @@ bool build_preset_scene(int preset, const std::string& asset_dir, int texture_mo
   if (preset != PRESET_BOX) {
     if (!tex("bunny/bunny.PPM", 1024, 1024, 3, t_bunny)) return false;
     int sub = detail > 0 ? std::min(detail + 3, 7) : 6;
-    Mesh bn = make_blob(sub);
+    Mesh bn;
+    if (!mesh("bunny/bunny.obj", bn, [&] { return make_blob(sub); })) return false;
     bake(bn, mk3(-1.5f, 0.2f, 1.2f), 0.25f);
     add_mesh(sc, bn, mat(MATL_REFRACTION, t_bunny), "bunny");
     // model 4: earth (reflection, white, translate(0,1,0)*scale(0.01))
-    Mesh e = make_sphere(64, 32);
+    Mesh e;
+    if (!mesh("earth/earth.obj", e, [] { return make_sphere(64, 32); })) return false;
     bake(e, mk3(0.0f, 1.0f, 0.0f), 0.01f);
     add_mesh(sc, e, mat(MATL_REFLECTION, t_white), "earth");
   }

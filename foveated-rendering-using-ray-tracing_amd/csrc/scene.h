@@ -46,8 +46,10 @@ enum ScenePreset { PRESET_BOX = 0, PRESET_BUNNY = 1, PRESET_VOKSELIA = 2 };
 
 // Builds a preset. texture_mode 0: load the reference assets from asset_dir (error if missing);
 // 1: deterministic procedural textures (same sizes), for asset-free tests.
+// mesh_mode 0: the reference's OBJ meshes where present under asset_dir, procedural stand-ins
+// otherwise; 1: procedural only; 2: OBJ required.
 bool build_preset_scene(int preset, const std::string& asset_dir, int texture_mode, float light_power,
-                        int detail, HostScene& out, std::string& err);
+                        int detail, HostScene& out, std::string& err, int mesh_mode = 0);
 
 bool load_ppm(const std::string& path, HostTexture& tex, std::string& err);
 bool load_hdr(const std::string& path, HostTexture& tex, std::string& err);

@@ -51,7 +51,7 @@ class fr_config(C.Structure):
                 ("spp", C.c_int), ("diffuse_max_depth", C.c_int), ("refraction_max_depth", C.c_int),
                 ("light_power", C.c_float), ("optimize", C.c_int), ("atrous_iterations", C.c_int),
                 ("write_extra", C.c_int), ("device", C.c_int), ("texture_mode", C.c_int), ("detail", C.c_int),
-                ("asset_dir", C.c_char_p)]
+                ("mesh_mode", C.c_int), ("asset_dir", C.c_char_p)]
 
 
 class fr_camera(C.Structure):
@@ -267,6 +267,7 @@ class Config:
     device: int = 0
     texture_mode: int = 0
     detail: int = 0
+    mesh_mode: int = 0  # 0: .obj meshes where present, else procedural; 1: procedural; 2: .obj required
     asset_dir: str = DEFAULT_ASSET_DIR
 
     def to_c(self) -> fr_config:

@@ -65,6 +65,8 @@ typedef struct fr_config {
   int device;                 /* HIP device ordinal */
   int texture_mode;           /* 0: reference assets from asset_dir (error if missing); 1: procedural */
   int detail;                 /* procedural mesh detail (0 = preset default) */
+  int mesh_mode;              /* 0: the reference's .obj meshes where present under asset_dir, procedural
+                               * stand-ins otherwise; 1: procedural only; 2: .obj required (FR_E_IO) */
   const char* asset_dir;      /* directory holding CedarCity.hdr, grid.ppm, bunny/bunny.PPM, ... */
 } fr_config;
 

@@ -186,3 +186,67 @@ def test_cpp_facade_driver_builds_and_fails_cleanly_without_gpu():
     import torch
     if not torch.cuda.is_available():
         assert r.returncode == 1 and "initialize failed" in r.stderr
+
+
+GROUND_OBJ = """# quad, 1-based and negative indices, v/vt/vn corners
+v -1 0 -1
+v 1 0 -1
+v 1 0 1
+v -1 0 1
+vt 0 0
+vt 1 0
+vt 1 1
+vt 0 1
+vn 0 1 0
+f -4/-4/-1 -3/-3/-1 -2/-2/-1 -1/-1/-1
+"""
+TETRA_OBJ = """o tetra
+v 0 0 0
+v 100 0 0
+v 0 100 0
+v 0 0 100
+vn 0 0 -1
+vn 0 -1 0
+vn -1 0 0
+vn 1 1 1
+f 1//1 3//1 2//1
+f 1//2 2//2 4//2
+f 1//3 4//3 3//3
+f 2//4 3//4 4//4
+"""
+
+
+def test_obj_meshes_replace_the_stand_ins(fovrt_mod, tmp_path):
+    """sutil::loadMesh semantics for the reference's models (FR/PathTracer.cpp:582-595): OBJ faces
+    fan-triangulated, the model transform baked into positions, normals by its inverse transpose."""
+    (tmp_path / "box").mkdir()
+    (tmp_path / "ground.obj").write_text(GROUND_OBJ)
+    (tmp_path / "box" / "box.obj").write_text(TETRA_OBJ)
+    cfg = fovrt_mod.Config(scene=fovrt_mod.SCENE_BOX, texture_mode=1, mesh_mode=2, asset_dir=str(tmp_path))
+    a = fovrt_mod.Scene(cfg).arrays()
+    assert len(a["flags"]) == 2 + 4
+    pos = np.asarray(a["pos"]).reshape(-1, 3, 3)
+    nrm = np.asarray(a["nrm"]).reshape(-1, 3, 3)
+    # ground: translate(0, -0.05, 0), quad (0,1,2),(0,2,3)
+    assert np.allclose(pos[0], [[-1, -0.05, -1], [1, -0.05, -1], [1, -0.05, 1]])
+    assert np.allclose(pos[1], [[-1, -0.05, -1], [1, -0.05, 1], [-1, -0.05, 1]])
+    assert np.allclose(np.asarray(a["uv"]).reshape(-1, 3, 2)[0], [[0, 0], [1, 0], [1, 1]])
+    # box: translate(-3.5, 0.2, 1.2) * scale(0.01) baked; normals / 0.01
+    assert np.allclose(pos[2], [[-3.5, 0.2, 1.2], [-3.5, 1.2, 1.2], [-2.5, 0.2, 1.2]], atol=1e-6)
+    assert np.allclose(nrm[2], [[0, 0, -100]] * 3)
+    flags = np.asarray(a["flags"])
+    assert (flags[:2] & 0x300).tolist() == [0x300, 0x300] and (flags[2:] & 0x300).tolist() == [0x100] * 4
+    # required but missing -> FR_E_IO; auto -> the procedural stand-in
+    with pytest.raises(fovrt_mod.FovrtError):
+        fovrt_mod.Scene(fovrt_mod.Config(scene=fovrt_mod.SCENE_BUNNY, texture_mode=1, mesh_mode=2,
+                                         asset_dir=str(tmp_path))).arrays()
+    auto = fovrt_mod.Scene(fovrt_mod.Config(scene=fovrt_mod.SCENE_BUNNY, texture_mode=1, mesh_mode=0,
+                                            asset_dir=str(tmp_path))).arrays()
+    assert len(auto["flags"]) > 10000  # OBJ ground + box, procedural bunny + earth
+    bad = tmp_path / "bad"
+    (bad / "box").mkdir(parents=True)
+    (bad / "ground.obj").write_text("v 0 0 0\nf 1 2 3\n")
+    (bad / "box" / "box.obj").write_text(TETRA_OBJ)
+    with pytest.raises(fovrt_mod.FovrtError):
+        fovrt_mod.Scene(fovrt_mod.Config(scene=fovrt_mod.SCENE_BOX, texture_mode=1, mesh_mode=2,
+                                         asset_dir=str(bad))).arrays()
