@@ -32,6 +32,7 @@ void launch_compaction(int, int, const unsigned long long*, const uint32_t*, uin
                        uint32_t*, hipStream_t);
 size_t compaction_tiles(int W, int H);
 void launch_shard_pack(const FrameUniforms&, const f4*, f4*, hipStream_t);
+void launch_logpolar(const f4*, f4*, f4*, int, int, f2, hipStream_t);
 void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
@@ -47,7 +48,7 @@ static thread_local std::string g_create_error;
 
 enum Phys {
   P_POSITION, P_NORMAL, P_DEPTH_A, P_DEPTH_B, P_DIFFUSE, P_WEIGHT, P_HIST_A, P_HIST_B, P_SHADING, P_EXTRA,
-  P_JFA_COORD, P_JFA_COLOR, P_SIBSON, P_PULLPUSH, P_ATROUS_A, P_ATROUS_B, P_COUNT
+  P_JFA_COORD, P_JFA_COLOR, P_SIBSON, P_PULLPUSH, P_ATROUS_A, P_ATROUS_B, P_LOGPOLAR, P_LOGPOLAR_INV, P_COUNT
 };
 
 struct fr_ctx {
@@ -566,6 +567,8 @@ static int resolve(fr_ctx* c, int id, int* phys) {
     case FR_BUF_SIBSON: *phys = P_SIBSON; return FR_OK;
     case FR_BUF_PULLPUSH: *phys = P_PULLPUSH; return FR_OK;
     case FR_BUF_ATROUS: *phys = c->atrous_out; return FR_OK;
+    case FR_BUF_LOGPOLAR: *phys = P_LOGPOLAR; return FR_OK;
+    case FR_BUF_LOGPOLAR_INVERSE: *phys = P_LOGPOLAR_INV; return FR_OK;
     default: return FR_E_INVALID;
   }
 }
@@ -631,6 +634,26 @@ static int ns_timed(fr_ctx* c, std::function<int()> f, uint64_t* ns) {
 int fr_jfa_render(fr_ctx* c, int in_buffer, uint64_t* ns) { if (!c) return FR_E_INVALID; return ns_timed(c, [&] { return enqueue_jfa(c, in_buffer); }, ns); }
 int fr_sibson_render(fr_ctx* c, uint64_t* ns) { if (!c) return FR_E_INVALID; return ns_timed(c, [&] { return enqueue_sibson(c); }, ns); }
 int fr_pullpush_render(fr_ctx* c, int in_buffer, uint64_t* ns) { if (!c) return FR_E_INVALID; return ns_timed(c, [&] { return enqueue_pullpush(c, in_buffer); }, ns); }
+static int enqueue_logpolar(fr_ctx* c, int in_buffer) {
+  int p;
+  if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "logpolar: bad input buffer");
+  if (p == P_LOGPOLAR || p == P_LOGPOLAR_INV) return fail(c, FR_E_INVALID, "logpolar: input is one of its outputs");
+  launch_logpolar(c->img[p], c->img[P_LOGPOLAR], c->img[P_LOGPOLAR_INV], c->W, c->H, c->U.gaze, c->stream);
+  return check_launch(c);
+}
+int fr_logpolar_render(fr_ctx* c, int in_buffer, uint64_t* ns) {
+  if (!c) return FR_E_INVALID;
+  return ns_timed(c, [&] { return enqueue_logpolar(c, in_buffer); }, ns);
+}
+
+int fr_set_gaze(fr_ctx* c, float x, float y) {
+  // cursorPosCallback (FR/gui.cpp:48-66) sets g_gaze in window coordinates (y down); the kernels
+  // use (g_gaze.x, H - g_gaze.y) (FR/PathTracer.cpp:796-797)
+  if (!c) return FR_E_INVALID;
+  c->U.gaze = mk2(x, (float)c->H - y);
+  return FR_OK;
+}
+
 int fr_atrous_render(fr_ctx* c, int count, int pos, int nrm, int col, uint64_t* ns) {
   if (!c) return FR_E_INVALID;
   return ns_timed(c, [&] { return enqueue_atrous(c, count, pos, nrm, col); }, ns);

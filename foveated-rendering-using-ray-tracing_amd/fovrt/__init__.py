@@ -38,6 +38,7 @@ class TextureName:
     """PathTracer::TextureName (FR/PathTracer.h:13-31) plus the reconstruction outputs."""
     POSITION, NORMAL, DEPTH, DIFFUSE, WEIGHT, THREAD, HISTORY, SHADING, EXTRA = range(9)
     JFA_COORD, JFA_COLOR, SIBSON, PULLPUSH, ATROUS, DEPTH_CACHE, HISTORY_CACHE, MASK = range(9, 17)
+    LOGPOLAR, LOGPOLAR_INVERSE = 17, 18
 
 
 class FovrtError(RuntimeError):
@@ -118,6 +119,8 @@ _SIGS = {
     "fr_sibson_render": [C.c_void_p, C.POINTER(C.c_uint64)],
     "fr_pullpush_render": [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)],
     "fr_atrous_render": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64)],
+    "fr_logpolar_render": [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)],
+    "fr_set_gaze": [C.c_void_p, C.c_float, C.c_float],
     "fr_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_trace_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_reconstruct_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
@@ -426,6 +429,10 @@ class PathTracer:
         """The reconstruction half of a frame (JFA -> Sibson -> pull-push -> A-Trous)."""
         return self._frame(_lib.fr_reconstruct_frame, timing)
 
+    def set_gaze(self, x, y):
+        """cursorPosCallback (FR/gui.cpp:48-66): gaze in window coordinates (y down)."""
+        self._check(_lib.fr_set_gaze(self._ctx, float(x), float(y)))
+
     # tile sharding of one view across ranks (include/fovrt.h, fr_set_shard)
     def set_shard(self, rank, count, tile=128):
         self._check(_lib.fr_set_shard(self._ctx, int(rank), int(count), int(tile)))
@@ -516,6 +523,17 @@ class JumpFlooding(_Pass):
     def render(self, rt=TextureName.SHADING):
         ns = C.c_uint64()
         self.tracer._check(_lib.fr_jfa_render(self.tracer._ctx, int(rt), C.byref(ns)))
+        return ns.value
+
+
+class LogPolarTransform(_Pass):
+    """LogPolarTransform::render(pt, query, elapsed, done) (FR/Log_Polar_Transform.cpp:40-106)."""
+    logPolarTex = TextureName.LOGPOLAR
+    ilogPolarTex = TextureName.LOGPOLAR_INVERSE
+
+    def render(self, pt=TextureName.PULLPUSH):
+        ns = C.c_uint64()
+        self.tracer._check(_lib.fr_logpolar_render(self.tracer._ctx, int(pt), C.byref(ns)))
         return ns.value
 
 

@@ -112,7 +112,9 @@ typedef enum fr_buffer_id {
   FR_BUF_DEPTH_CACHE = 14,
   FR_BUF_HISTORY_CACHE = 15,
   FR_BUF_MASK = 16,         /* u8 usingRay per pixel */
-  FR_BUF_COUNT = 17
+  FR_BUF_LOGPOLAR = 17,     /* LogPolarTransform::logPolarTex  (forward image, W/4 x H/4 used) */
+  FR_BUF_LOGPOLAR_INVERSE = 18, /* LogPolarTransform::ilogPolarTex */
+  FR_BUF_COUNT = 19
 } fr_buffer_id;
 
 typedef enum fr_format { FR_FMT_RGBA32F = 0, FR_FMT_U32 = 1, FR_FMT_U8 = 2 } fr_format;
@@ -188,6 +190,13 @@ int fr_sibson_render(fr_ctx* ctx, uint64_t* elapsed_ns);                        
 int fr_pullpush_render(fr_ctx* ctx, int in_buffer, uint64_t* elapsed_ns);       /* PullPushInterpolation::render */
 int fr_atrous_render(fr_ctx* ctx, int count, int pos_buffer, int nrm_buffer, int col_buffer,
                      uint64_t* elapsed_ns);                                     /* ATrous::render */
+
+/* LogPolarTransform::render (FR/Log_Polar_Transform.cpp:40-106) of any RGBA32F buffer around the
+ * current gaze: forward image -> FR_BUF_LOGPOLAR, round trip -> FR_BUF_LOGPOLAR_INVERSE. */
+int fr_logpolar_render(fr_ctx* ctx, int in_buffer, uint64_t* elapsed_ns);
+/* Gaze input (cursorPosCallback, FR/gui.cpp:48-66): window coordinates, y down; the kernels use
+ * (x, H - y) from the next launch on (also replaced by fr_set_camera's gaze). */
+int fr_set_gaze(fr_ctx* ctx, float x, float y);
 
 /* The whole main.cpp loop body (update -> 0 -> 1 -> 2 -> 3 -> JFA -> SI -> PPI -> AT), enqueued on the
  * context stream. timing may be NULL (no host synchronisation then; call fr_synchronize). */

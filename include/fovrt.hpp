@@ -154,6 +154,9 @@ class PathTracer {
     check(fr_gaze_target(ctx(), g.data()), ctx_, "gaze_target");
     return g;
   }
+  void set_gaze(float x, float y) {  // cursorPosCallback (FR/gui.cpp:48-66): window coordinates, y down
+    check(fr_set_gaze(ctx(), x, y), ctx_, "set_gaze");
+  }
   unsigned int ray_count() {  // m_context["ray_count"] (FR/main.cpp:288-299)
     uint32_t n = 0;
     check(fr_ray_count(ctx(), &n), ctx_, "ray_count");
@@ -202,6 +205,22 @@ class JumpFlooding {
   void resetShader() {}
   const Texture coordTex{FR_BUF_JFA_COORD};
   const Texture colorTex{FR_BUF_JFA_COLOR};
+
+ private:
+  PathTracer& t_;
+};
+
+class LogPolarTransform {  // FR/Log_Polar_Transform.h
+ public:
+  explicit LogPolarTransform(PathTracer& t) : t_(t) {}
+  void render(Texture pt, const unsigned* = nullptr, uint64_t* elapsed_time = nullptr, int* done = nullptr) {
+    uint64_t ns = 0;
+    check(fr_logpolar_render(t_.ctx(), pt.id, &ns), t_.ctx(), "LogPolarTransform::render");
+    detail::finish(ns, elapsed_time, done);
+  }
+  void resetShader() {}
+  const Texture logPolarTex{FR_BUF_LOGPOLAR};
+  const Texture ilogPolarTex{FR_BUF_LOGPOLAR_INVERSE};
 
  private:
   PathTracer& t_;

@@ -52,6 +52,7 @@ def lib():
         L.or_sibson.argtypes = [C.c_int, C.c_int, F, F, F]
         L.or_pullpush.argtypes = [C.c_int, C.c_int, F, F, F, F]
         L.or_atrous.argtypes = [C.c_int, C.c_int, C.c_int, F, F, F, F]
+        L.or_logpolar.argtypes = [C.c_int, C.c_int, C.c_float, C.c_float, F, F, F]
         _lib = L
     return _lib
 
@@ -204,3 +205,14 @@ def atrous(count, pos, nrm, col):
     out = np.empty_like(col)
     lib().or_atrous(W, H, count, fp(pos), fp(nrm), fp(col), fp(out))
     return out
+
+
+def logpolar(img, gaze, fwd=None, inv=None):
+    """LogPolarTransform::render of img around gaze = (x, y) (kernel coordinates); fwd / inv are the
+    persistent output textures (zeros if None). Returns (fwd, inv)."""
+    img = _c(img, np.float32)
+    H, W = img.shape[:2]
+    fwd = np.zeros((H, W, 4), np.float32) if fwd is None else _c(fwd, np.float32).copy()
+    inv = np.zeros((H, W, 4), np.float32) if inv is None else _c(inv, np.float32).copy()
+    lib().or_logpolar(W, H, float(gaze[0]), float(gaze[1]), fp(img), fp(fwd), fp(inv))
+    return fwd, inv

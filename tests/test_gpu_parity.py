@@ -316,3 +316,26 @@ def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile):
         assert equal_nan(root.read(tid), full.read(tid)), tid
     masks = sum(t.read(TN.MASK).astype(np.int32) for t in ranks)
     assert np.array_equal(masks, full.read(TN.MASK))  # the ranks' masks partition the full mask
+
+
+# ---------------------------------------------------------------------------------------------
+# LogPolarTransform (FR/Log_Polar_Transform.cpp:40-106) and the gaze input (FR/gui.cpp:48-66)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("W,H", [(128, 96), (200, 136)])
+def test_logpolar_transform_bit_exact(fovrt_mod, oracle, W, H):
+    t = _box_tracer(fovrt_mod, W, H)
+    rs = np.random.RandomState(W)
+    lp = fovrt_mod.LogPolarTransform(t)
+    fwd = inv = None
+    for k, gaze_window in enumerate([None, (W * 0.3, H * 0.2), (W - 5.0, 7.0)]):
+        img = rs.rand(H, W, 4).astype(np.float32)
+        t.write(TN.SHADING, img)
+        if gaze_window is None:
+            gaze = (W // 2, H - H // 2)  # the default gaze (FR/gui.cpp:34-35, kernels use H - y)
+        else:
+            t.set_gaze(*gaze_window)
+            gaze = (np.float32(gaze_window[0]), np.float32(H) - np.float32(gaze_window[1]))
+        lp.render(TN.SHADING)
+        fwd, inv = oracle.logpolar(img, gaze, fwd, inv)  # outputs persist across calls, as GL textures do
+        assert equal_nan(t.read(TN.LOGPOLAR), fwd), k
+        assert equal_nan(t.read(TN.LOGPOLAR_INVERSE), inv), k
