@@ -179,6 +179,9 @@ def main():
                     help="views rendered by the job (0: one per rank = weak scaling); the ranks of a view "
                          "tile-shard it and gather the tiles to the view's first rank for reconstruction")
     ap.add_argument("--tile", type=int, default=128, help="screen tile size of the tile sharding")
+    ap.add_argument("--composite", action="store_true",
+                    help="every frame, gather the views' reconstructed images to rank 0 over RCCL and compose them "
+                         "side by side (the final composite of the stereo configuration)")
     args = ap.parse_args()
     args.mask = fovrt.MASKS[args.mask]
     scene = fovrt.SCENES[args.scene]
@@ -212,6 +215,9 @@ def main():
     views = args.views or world
     view, vrank, G = view_layout(rank, world, views)
     groups = make_view_groups(dist, world, views) if dist is not None and G > 1 else None
+    # the first rank of every view, for the final composite on rank 0
+    roots_group = (dist.new_group([v * (world // views) for v in range(views)])
+                   if dist is not None and args.composite and views > 1 else None)
     cfg = fovrt.Config(width=W, height=H, scene=scene, mask_mode=args.mask, spp=args.spp, diffuse_max_depth=args.dmd,
                        refraction_max_depth=args.refraction_max_depth, device=device)
     tracer = fovrt.PathTracer(cfg)
@@ -233,9 +239,32 @@ def main():
         nbytes = n_tex * 16
         root = view * G
 
+    comp_img = comp_list = comp_out = None
+    if roots_group is not None and vrank == 0:
+        comp_img = torch.empty(W * H * 4, dtype=torch.float32, device=f"cuda:{device}")
+        if rank == 0:
+            comp_stack = torch.empty(views * W * H * 4, dtype=torch.float32, device=f"cuda:{device}")
+            comp_list = list(comp_stack.chunk(views))  # the gather lands the views consecutively
+            comp_out = torch.empty_like(comp_stack)
+
+    def composite():
+        """Final composite: view roots send their A-Trous image to rank 0, which lays them side by side."""
+        if comp_img is None:
+            return
+        tracer.copy_buffer(fovrt.TextureName.ATROUS, comp_img.data_ptr(), W * H * 16)
+        gather_slabs(dist, roots_group, comp_img, comp_list, 0)
+        if rank == 0:
+            sync()
+            tracer.composite_views(comp_list[0].data_ptr(), views, comp_out.data_ptr(), comp_out.numel() * 4)
+
     def step(timing):
         """One frame of the view: the whole chain on one rank, or trace -> pack -> gather -> (root)
-        unpack + reconstruct when the view is tile-sharded."""
+        unpack + reconstruct when the view is tile-sharded; then the optional final composite."""
+        tm = view_frame(timing)
+        composite()
+        return tm
+
+    def view_frame(timing):
         if G == 1:
             return tracer.frame(timing=timing)
         tm = tracer.trace_frame(timing=timing)
@@ -313,6 +342,7 @@ def main():
                                "JFA + Sibson + pull-push + A-Trous",
                    "scene": args.scene, "width": W, "height": H, "spp": args.spp, "diffuse_max_depth": args.dmd,
                    "mask_mode": args.mask, "foveal_density": round(rho, 5), "views": views,
+                   "composite": bool(args.composite and views > 1),
                    "parallelism": (f"views x{world} (one view per GPU)" if G == 1 else
                                    f"{views} view(s) x {G}-way {args.tile}px tile sharding, RCCL gather to the "
                                    f"view's first rank"),

@@ -33,6 +33,7 @@ void launch_compaction(int, int, const unsigned long long*, const uint32_t*, uin
 size_t compaction_tiles(int W, int H);
 void launch_shard_pack(const FrameUniforms&, const f4*, f4*, hipStream_t);
 void launch_logpolar(const f4*, f4*, f4*, int, int, f2, hipStream_t);
+void launch_composite(const f4*, int, int, int, f4*, hipStream_t);
 void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
@@ -644,6 +645,29 @@ static int enqueue_logpolar(fr_ctx* c, int in_buffer) {
 int fr_logpolar_render(fr_ctx* c, int in_buffer, uint64_t* ns) {
   if (!c) return FR_E_INVALID;
   return ns_timed(c, [&] { return enqueue_logpolar(c, in_buffer); }, ns);
+}
+
+int fr_copy_buffer(fr_ctx* c, int id, void* dst, size_t bytes) {
+  fr_buffer_view v;
+  int rc = fr_get_buffer(c, id, &v);
+  if (rc) return rc;
+  if (!dst || bytes > v.bytes) return fail(c, FR_E_INVALID, "copy_buffer: size");
+  hipSetDevice(c->cfg.device);
+  HIP_TRY(c, hipMemcpyAsync(dst, v.device_ptr, bytes, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FR_OK;
+}
+
+int fr_composite_views(fr_ctx* c, const void* views, int nviews, void* out, size_t out_bytes) {
+  if (!c || !views || !out || nviews < 1) return FR_E_INVALID;
+  const size_t need = (size_t)nviews * c->W * c->H * sizeof(f4);
+  if (out_bytes < need) return fail(c, FR_E_INVALID, "fr_composite_views: output smaller than nviews * W * H * 16");
+  hipSetDevice(c->cfg.device);
+  launch_composite((const f4*)views, nviews, c->W, c->H, (f4*)out, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FR_OK;
 }
 
 int fr_set_gaze(fr_ctx* c, float x, float y) {

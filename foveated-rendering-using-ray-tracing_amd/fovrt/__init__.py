@@ -121,6 +121,7 @@ _SIGS = {
     "fr_atrous_render": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64)],
     "fr_logpolar_render": [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)],
     "fr_set_gaze": [C.c_void_p, C.c_float, C.c_float],
+    "fr_composite_views": [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_trace_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_reconstruct_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
@@ -132,6 +133,7 @@ _SIGS = {
     "fr_get_buffer": [C.c_void_p, C.c_int, C.POINTER(fr_buffer_view)],
     "fr_read_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_write_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
+    "fr_copy_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_get_stats": [C.c_void_p, C.POINTER(fr_stats)],
     "fr_reset_stats": [C.c_void_p],
     "fr_scene_export": [C.c_void_p, C.POINTER(fr_scene_arrays)],
@@ -428,6 +430,15 @@ class PathTracer:
     def reconstruct_frame(self, timing=True):
         """The reconstruction half of a frame (JFA -> Sibson -> pull-push -> A-Trous)."""
         return self._frame(_lib.fr_reconstruct_frame, timing)
+
+    def copy_buffer(self, buffer_id, device_ptr, nbytes):
+        """Device-to-device copy of a buffer into memory the caller owns (e.g. a torch tensor)."""
+        self._check(_lib.fr_copy_buffer(self._ctx, int(buffer_id), C.c_void_p(device_ptr), int(nbytes)))
+
+    def composite_views(self, views_ptr, nviews, out_ptr, out_bytes):
+        """Side-by-side composite of nviews W x H device images into (nviews W) x H (device pointers)."""
+        self._check(_lib.fr_composite_views(self._ctx, C.c_void_p(views_ptr), int(nviews), C.c_void_p(out_ptr),
+                                            int(out_bytes)))
 
     def set_gaze(self, x, y):
         """cursorPosCallback (FR/gui.cpp:48-66): gaze in window coordinates (y down)."""

@@ -194,6 +194,10 @@ int fr_atrous_render(fr_ctx* ctx, int count, int pos_buffer, int nrm_buffer, int
 /* LogPolarTransform::render (FR/Log_Polar_Transform.cpp:40-106) of any RGBA32F buffer around the
  * current gaze: forward image -> FR_BUF_LOGPOLAR, round trip -> FR_BUF_LOGPOLAR_INVERSE. */
 int fr_logpolar_render(fr_ctx* ctx, int in_buffer, uint64_t* elapsed_ns);
+/* Final composite of nviews rendered views (e.g. the two eyes gathered to one GPU over RCCL):
+ * device `views` = nviews consecutive W x H RGBA32F images -> device `out` = (nviews * W) x H,
+ * view v in columns [v W, (v+1) W) (renderAll's side-by-side display, FR/main.cpp:26-113). */
+int fr_composite_views(fr_ctx* ctx, const void* views, int nviews, void* out, size_t out_bytes);
 /* Gaze input (cursorPosCallback, FR/gui.cpp:48-66): window coordinates, y down; the kernels use
  * (x, H - y) from the next launch on (also replaced by fr_set_camera's gaze). */
 int fr_set_gaze(fr_ctx* ctx, float x, float y);
@@ -222,6 +226,7 @@ int fr_shard_unpack(fr_ctx* ctx, int buffer_id, int src_rank, const void* device
 int fr_get_buffer(fr_ctx* ctx, int id, fr_buffer_view* view);
 int fr_read_buffer(fr_ctx* ctx, int id, void* host, size_t bytes);
 int fr_write_buffer(fr_ctx* ctx, int id, const void* host, size_t bytes);
+int fr_copy_buffer(fr_ctx* ctx, int id, void* device_dst, size_t bytes);  /* device-to-device, synchronous */
 
 int fr_get_stats(fr_ctx* ctx, fr_stats* stats);
 int fr_reset_stats(fr_ctx* ctx);

@@ -5,6 +5,6 @@ set -eo pipefail
 export FOVRT_DIST_BACKEND=gloo
 A="--steps 3 --warmup 1 --width 1920 --height 1080 --no-cpu-baseline"
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-  --master-port 29511 bench.py $A --views 2 > gpurun_out/rehearse_views.log 2>&1
+  --master-port 29511 bench.py $A --views 2 --composite > gpurun_out/rehearse_views.log 2>&1
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29512 bench.py $A --views 1 --tile 128 > gpurun_out/rehearse_tiles.log 2>&1

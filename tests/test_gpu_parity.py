@@ -339,3 +339,23 @@ def test_logpolar_transform_bit_exact(fovrt_mod, oracle, W, H):
         fwd, inv = oracle.logpolar(img, gaze, fwd, inv)  # outputs persist across calls, as GL textures do
         assert equal_nan(t.read(TN.LOGPOLAR), fwd), k
         assert equal_nan(t.read(TN.LOGPOLAR_INVERSE), inv), k
+
+
+def test_composite_views_side_by_side(fovrt_mod):
+    import torch
+    W, H = 96, 64
+    eyes = [make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=1, dmd=1) for _ in range(2)]
+    for k, t in enumerate(eyes):
+        cam = fovrt_mod.Camera.preset(1, W, H)
+        cam.setPosition(np.asarray(cam.pos) + np.array([0.064 * (k - 0.5), 0, 0], np.float32))
+        cam.lookAt(cam.target)
+        t.update_optix_variables(cam)
+        t.frame(timing=False)
+    stack = torch.empty(2 * W * H * 4, dtype=torch.float32, device="cuda")
+    for k, t in enumerate(eyes):
+        t.copy_buffer(TN.ATROUS, stack[k * W * H * 4:].data_ptr(), W * H * 16)
+    out = torch.empty_like(stack)
+    eyes[0].composite_views(stack.data_ptr(), 2, out.data_ptr(), out.numel() * 4)
+    img = out.cpu().numpy().reshape(H, 2 * W, 4)
+    assert equal_nan(img[:, :W], eyes[0].read(TN.ATROUS)) and equal_nan(img[:, W:], eyes[1].read(TN.ATROUS))
+    assert not equal_nan(img[:, :W], img[:, W:])  # two different eyes
