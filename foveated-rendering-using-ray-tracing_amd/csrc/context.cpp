@@ -20,7 +20,7 @@
 namespace fr {
 void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
 void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
-                        const f4*, uint32_t*, f4*, DevStats*, int, hipStream_t);
+                        const f4*, uint32_t*, f4*, DevStats*, hipStream_t);
 void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
                           const f4*, f4*, f4*, hipStream_t);
 size_t shade_counter_words();
@@ -95,7 +95,6 @@ struct fr_ctx {
   bool mask_dirty = false;
   hipEvent_t ev[12] = {};
   bool time_kernels = false;  // fr_frame with timing: also time the path-trace kernel alone
-  int wait_threshold = 64;    // lanes (of 64) waiting before a wave leaves its traversal steps to shade (64: all)
   // scene export copies
   std::vector<const float*> tex_ptrs;
   std::vector<int32_t> tex_dims, mat_pairs;
@@ -335,7 +334,6 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
 
   fr_ctx* c = new fr_ctx();
   c->cfg = cfg;
-  if (const char* w = getenv("FOVRT_WAIT_THRESHOLD")) c->wait_threshold = std::max(1, std::min(64, atoi(w)));
   c->asset_dir = cfg.asset_dir ? cfg.asset_dir : "assets";
   c->cfg.asset_dir = nullptr;
   c->W = cfg.width; c->H = cfg.height;
@@ -540,7 +538,7 @@ static int enqueue_shading(fr_ctx* c) {
   const uint32_t N = (uint32_t)((size_t)c->W * c->H);
   if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
   launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache],
-                     c->shade_ctr, c->samples, c->stats, c->wait_threshold, c->stream);
+                     c->shade_ctr, c->samples, c->stats, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache], c->samples,
                        c->img[c->hist_cur], c->img[P_SHADING], c->stream);
