@@ -58,6 +58,7 @@ struct fr_ctx {
   std::string err;
   int W = 0, H = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // fr_frame: pull-push + A-Trous run beside JFA + Sibson
   HostScene scene;
   Bvh bvh;
   // device scene
@@ -93,7 +94,7 @@ struct fr_ctx {
   bool light_pending = false;
   bool compacted = false;
   bool mask_dirty = false;
-  hipEvent_t ev[12] = {};
+  hipEvent_t ev[16] = {};
   bool time_kernels = false;  // fr_frame with timing: also time the path-trace kernel alone
   // scene export copies
   std::vector<const float*> tex_ptrs;
@@ -339,7 +340,11 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   c->W = cfg.width; c->H = cfg.height;
   auto bail = [&](int code) { g_create_error = c->err; fr_destroy(c); return code; };
   if (hipSetDevice(cfg.device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(FR_E_HIP); }
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { c->err = "stream create failed"; return bail(FR_E_HIP); }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+    c->err = "stream create failed";
+    return bail(FR_E_HIP);
+  }
   for (auto& e : c->ev) hipEventCreate(&e);
 
   std::string err;
@@ -454,6 +459,7 @@ int fr_destroy(fr_ctx* c) {
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
+  if (c->stream2) hipStreamDestroy(c->stream2);
   delete c;
   return FR_OK;
 }
@@ -582,25 +588,26 @@ static int enqueue_sibson(fr_ctx* c) {
   launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, c->stream);
   return check_launch(c);
 }
-static int enqueue_pullpush(fr_ctx* c, int in_buffer) {
+static int enqueue_pullpush(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {
   int p;
   if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "pullpush: bad input buffer");
-  launch_pullpush(c->img[p], c->pull, c->push, c->snap, c->img[P_PULLPUSH], c->W, c->H, c->stream);
+  launch_pullpush(c->img[p], c->pull, c->push, c->snap, c->img[P_PULLPUSH], c->W, c->H, stream ? stream : c->stream);
   return check_launch(c);
 }
-static int enqueue_atrous(fr_ctx* c, int count, int pos, int nrm, int col) {
+static int enqueue_atrous(fr_ctx* c, int count, int pos, int nrm, int col, hipStream_t stream = nullptr) {
+  if (!stream) stream = c->stream;
   int pp, pn, pc;
   if (count < 1 || resolve(c, pos, &pp) || resolve(c, nrm, &pn) || resolve(c, col, &pc))
     return fail(c, FR_E_INVALID, "atrous: bad arguments");
   if (pc == P_ATROUS_A || pc == P_ATROUS_B) return fail(c, FR_E_INVALID, "atrous: colour input aliases the output");
   float c_phi = 1.f, n_phi = 1.f, p_phi = 1.f;
   int sw = 1;
-  launch_atrous(c->img[pp], c->img[pn], c->img[pc], c->img[P_ATROUS_A], c->W, c->H, c_phi, n_phi, p_phi, (float)sw, c->stream);
+  launch_atrous(c->img[pp], c->img[pn], c->img[pc], c->img[P_ATROUS_A], c->W, c->H, c_phi, n_phi, p_phi, (float)sw, stream);
   bool usingA = true;
   for (int k = 1; k < count; k++) {  // FR/ATrous.cpp:90-113
     c_phi *= 1.0f; n_phi *= 0.5f; p_phi *= 1.0f; sw *= 2;
-    if (usingA) launch_atrous(c->img[pp], c->img[pn], c->img[P_ATROUS_A], c->img[P_ATROUS_B], c->W, c->H, c_phi, n_phi, p_phi, (float)sw, c->stream);
-    else launch_atrous(c->img[pp], c->img[pn], c->img[P_ATROUS_B], c->img[P_ATROUS_A], c->W, c->H, c_phi, n_phi, p_phi, (float)sw, c->stream);
+    if (usingA) launch_atrous(c->img[pp], c->img[pn], c->img[P_ATROUS_A], c->img[P_ATROUS_B], c->W, c->H, c_phi, n_phi, p_phi, (float)sw, stream);
+    else launch_atrous(c->img[pp], c->img[pn], c->img[P_ATROUS_B], c->img[P_ATROUS_A], c->W, c->H, c_phi, n_phi, p_phi, (float)sw, stream);
     usingA = !usingA;
   }
   c->atrous_out = usingA ? P_ATROUS_A : P_ATROUS_B;
@@ -708,15 +715,28 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
   }
   if (t) hipEventRecord(ev[4], c->stream);
   if (recon) {
+    // two independent chains read the shading: JFA -> Sibson, and pull-push -> A-Trous (atFS binds
+    // the JFA texture but never reads it, FR/shader/atFS.glsl:40-90); the second runs on stream2
+    hipEventRecord(ev[11], c->stream);
+    hipStreamWaitEvent(c->stream2, ev[11], 0);
+    if (t) hipEventRecord(ev[13], c->stream2);
+    if ((rc = enqueue_pullpush(c, FR_BUF_SHADING, c->stream2))) return rc;
+    if (t) hipEventRecord(ev[14], c->stream2);
+    if ((rc = enqueue_atrous(c, c->cfg.atrous_iterations, FR_BUF_POSITION, FR_BUF_NORMAL, FR_BUF_PULLPUSH,
+                             c->stream2))) return rc;
+    if (t) hipEventRecord(ev[15], c->stream2);
+    hipEventRecord(ev[12], c->stream2);
     if ((rc = enqueue_jfa(c, FR_BUF_SHADING))) return rc;
     if (t) hipEventRecord(ev[5], c->stream);
     if ((rc = enqueue_sibson(c))) return rc;
     if (t) hipEventRecord(ev[6], c->stream);
-    if ((rc = enqueue_pullpush(c, FR_BUF_SHADING))) return rc;
+    hipStreamWaitEvent(c->stream, ev[12], 0);  // join: the next launch on the context stream sees both
     if (t) hipEventRecord(ev[7], c->stream);
-    if ((rc = enqueue_atrous(c, c->cfg.atrous_iterations, FR_BUF_POSITION, FR_BUF_NORMAL, FR_BUF_PULLPUSH))) return rc;
   } else if (t) {
     for (int i = 5; i <= 7; i++) hipEventRecord(ev[i], c->stream);
+    hipEventRecord(ev[13], c->stream);
+    hipEventRecord(ev[14], c->stream);
+    hipEventRecord(ev[15], c->stream);
   }
   if (t) {
     hipEventRecord(ev[8], c->stream);
@@ -728,8 +748,8 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     t->shading_ms = elapsed(ev[3], ev[4]);
     t->jfa_ms = elapsed(ev[4], ev[5]);
     t->sibson_ms = elapsed(ev[5], ev[6]);
-    t->pullpush_ms = elapsed(ev[6], ev[7]);
-    t->atrous_ms = elapsed(ev[7], ev[8]);
+    t->pullpush_ms = elapsed(ev[13], ev[14]);
+    t->atrous_ms = elapsed(ev[14], ev[15]);
     t->total_ms = elapsed(ev[0], ev[8]);
     t->shade_paths_ms = elapsed(ev[9], ev[10]);
     hipMemcpy(&t->ray_count, c->ray_count, 4, hipMemcpyDeviceToHost);
