@@ -49,7 +49,9 @@ static thread_local std::string g_create_error;
 
 enum Phys {
   P_POSITION, P_NORMAL, P_DEPTH_A, P_DEPTH_B, P_DIFFUSE, P_WEIGHT, P_HIST_A, P_HIST_B, P_SHADING, P_EXTRA,
-  P_JFA_COORD, P_JFA_COLOR, P_SIBSON, P_PULLPUSH, P_ATROUS_A, P_ATROUS_B, P_LOGPOLAR, P_LOGPOLAR_INV, P_COUNT
+  P_JFA_COORD, P_JFA_COLOR, P_SIBSON, P_PULLPUSH, P_ATROUS_A, P_ATROUS_B, P_LOGPOLAR, P_LOGPOLAR_INV,
+  P_POSITION_B, P_NORMAL_B, P_SHADING_B,  // frame-parity partners of the buffers the reconstruction reads
+  P_COUNT
 };
 
 struct fr_ctx {
@@ -58,7 +60,13 @@ struct fr_ctx {
   std::string err;
   int W = 0, H = 0;
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // fr_frame: pull-push + A-Trous run beside JFA + Sibson
+  hipStream_t stream2 = nullptr;  // reconstruction chain 2: pull-push -> A-Trous
+  hipStream_t stream3 = nullptr;  // reconstruction chain 1: JFA -> Sibson
+  // Frame pipelining: frame N's reconstruction (stream3 + stream2) runs while frame N+1 traces on
+  // `stream`. The buffers the reconstruction reads (POSITION, NORMAL, SHADING) alternate by frame
+  // parity `par`; the trace half of a frame waits for the reconstruction that last read its parity.
+  int par = 0;
+  bool recon_pending[2] = {false, false};
   HostScene scene;
   Bvh bvh;
   // device scene
@@ -94,7 +102,8 @@ struct fr_ctx {
   bool light_pending = false;
   bool compacted = false;
   bool mask_dirty = false;
-  hipEvent_t ev[16] = {};
+  hipEvent_t ev[24] = {};  // 0-15 stage timing; 16 fork; 17 chain-2 join; 18, 19 reconstruction done per parity;
+                           // 20-22 chain-1 timing
   bool time_kernels = false;  // fr_frame with timing: also time the path-trace kernel alone
   // scene export copies
   std::vector<const float*> tex_ptrs;
@@ -341,7 +350,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   auto bail = [&](int code) { g_create_error = c->err; fr_destroy(c); return code; };
   if (hipSetDevice(cfg.device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(FR_E_HIP); }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
     c->err = "stream create failed";
     return bail(FR_E_HIP);
   }
@@ -450,6 +460,8 @@ int fr_destroy(fr_ctx* c) {
   if (!c) return FR_E_INVALID;
   hipSetDevice(c->cfg.device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->stream2) hipStreamSynchronize(c->stream2);
+  if (c->stream3) hipStreamSynchronize(c->stream3);
   auto fr = [](void* p) { if (p) hipFree(p); };
   fr(c->d_nodes); fr(c->d_tri); fr(c->d_prim); fr(c->d_shade);
   for (auto p : c->d_tex) fr(p);
@@ -460,6 +472,7 @@ int fr_destroy(fr_ctx* c) {
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   if (c->stream2) hipStreamDestroy(c->stream2);
+  if (c->stream3) hipStreamDestroy(c->stream3);
   delete c;
   return FR_OK;
 }
@@ -500,7 +513,24 @@ int fr_accum_frame(fr_ctx* c, uint32_t* f) {
   return FR_OK;
 }
 
+static int P_pos(const fr_ctx* c) { return c->par ? P_POSITION_B : P_POSITION; }
+static int P_nrm(const fr_ctx* c) { return c->par ? P_NORMAL_B : P_NORMAL; }
+static int P_shd(const fr_ctx* c) { return c->par ? P_SHADING_B : P_SHADING; }
+
+// The context stream waits for every reconstruction still in flight (before any call that reads or
+// writes what the reconstruction uses, or hands buffers to the caller).
+static void join_recon(fr_ctx* c) {
+  for (int k = 0; k < 2; k++)
+    if (c->recon_pending[k]) { hipStreamWaitEvent(c->stream, c->ev[18 + k], 0); c->recon_pending[k] = false; }
+}
+
 static int enqueue_geometry(fr_ctx* c) {
+  // a new frame: switch to the other parity, once the reconstruction that read it has finished
+  c->par ^= 1;
+  if (c->recon_pending[c->par]) {
+    hipStreamWaitEvent(c->stream, c->ev[18 + c->par], 0);
+    c->recon_pending[c->par] = false;
+  }
   // frame = m_accumFrame++ ; a light change resets the counter afterwards (FR/PathTracer.cpp:99-116)
   c->U.frame = c->accum++;
   if (c->light_pending) { c->light_pending = false; c->accum = 0; }
@@ -509,7 +539,7 @@ static int enqueue_geometry(fr_ctx* c) {
     hipMemsetAsync(c->img[c->hist_cur], 0, bytes, c->stream);
     hipMemsetAsync(c->img[c->hist_cache], 0, bytes, c->stream);
   }
-  launch_gbuffer(c->dsc, c->U, c->img[P_POSITION], c->img[P_NORMAL], c->img[c->depth_cur], c->img[P_DIFFUSE],
+  launch_gbuffer(c->dsc, c->U, c->img[P_pos(c)], c->img[P_nrm(c)], c->img[c->depth_cur], c->img[P_DIFFUSE],
                  c->img[P_WEIGHT], c->gclass, c->stats, c->stream);
   c->compacted = false;
   return check_launch(c);
@@ -517,8 +547,8 @@ static int enqueue_geometry(fr_ctx* c) {
 
 static int enqueue_sampling(fr_ctx* c) {
   c->mask_dirty = false;
-  launch_sampling(c->U, c->dsc, c->img[P_POSITION], c->img[c->depth_cur], c->img[c->depth_cache], c->img[P_WEIGHT],
-                  c->img[P_NORMAL], c->img[P_DIFFUSE], c->img[P_EXTRA], c->mask, c->gclass, c->words, c->counts,
+  launch_sampling(c->U, c->dsc, c->img[P_pos(c)], c->img[c->depth_cur], c->img[c->depth_cache], c->img[P_WEIGHT],
+                  c->img[P_nrm(c)], c->img[P_DIFFUSE], c->img[P_EXTRA], c->mask, c->gclass, c->words, c->counts,
                   c->cfg.write_extra, c->stream);
   c->compacted = false;
   return check_launch(c);
@@ -540,14 +570,14 @@ static int enqueue_shading(fr_ctx* c) {
     if (rc) return rc;
   }
   launch_carry_history(c->U, c->mask, c->img[P_WEIGHT], c->img[c->hist_cache], c->img[c->hist_cur],
-                       c->img[P_SHADING], c->stream);
+                       c->img[P_shd(c)], c->stream);
   const uint32_t N = (uint32_t)((size_t)c->W * c->H);
   if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
   launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache],
                      c->shade_ctr, c->samples, c->stats, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache], c->samples,
-                       c->img[c->hist_cur], c->img[P_SHADING], c->stream);
+                       c->img[c->hist_cur], c->img[P_shd(c)], c->stream);
   int rc = check_launch(c);
   // swapBuffer("history_cache", "history_buffer"); swapBuffer("depth_cache", "depth_buffer") (:226-227)
   std::swap(c->hist_cur, c->hist_cache);
@@ -557,15 +587,15 @@ static int enqueue_shading(fr_ctx* c) {
 
 static int resolve(fr_ctx* c, int id, int* phys) {
   switch (id) {
-    case FR_BUF_POSITION: *phys = P_POSITION; return FR_OK;
-    case FR_BUF_NORMAL: *phys = P_NORMAL; return FR_OK;
+    case FR_BUF_POSITION: *phys = P_pos(c); return FR_OK;
+    case FR_BUF_NORMAL: *phys = P_nrm(c); return FR_OK;
     case FR_BUF_DEPTH: *phys = c->depth_cur; return FR_OK;
     case FR_BUF_DEPTH_CACHE: *phys = c->depth_cache; return FR_OK;
     case FR_BUF_DIFFUSE: *phys = P_DIFFUSE; return FR_OK;
     case FR_BUF_WEIGHT: *phys = P_WEIGHT; return FR_OK;
     case FR_BUF_HISTORY: *phys = c->hist_cur; return FR_OK;
     case FR_BUF_HISTORY_CACHE: *phys = c->hist_cache; return FR_OK;
-    case FR_BUF_SHADING: *phys = P_SHADING; return FR_OK;
+    case FR_BUF_SHADING: *phys = P_shd(c); return FR_OK;
     case FR_BUF_EXTRA: *phys = P_EXTRA; return FR_OK;
     case FR_BUF_JFA_COORD: *phys = P_JFA_COORD; return FR_OK;
     case FR_BUF_JFA_COLOR: *phys = P_JFA_COLOR; return FR_OK;
@@ -578,14 +608,15 @@ static int resolve(fr_ctx* c, int id, int* phys) {
   }
 }
 
-static int enqueue_jfa(fr_ctx* c, int in_buffer) {
+static int enqueue_jfa(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {
   int p;
   if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "jfa: bad input buffer");
-  launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->W, c->H, c->stream);
+  launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->W, c->H,
+             stream ? stream : c->stream);
   return check_launch(c);
 }
-static int enqueue_sibson(fr_ctx* c) {
-  launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, c->stream);
+static int enqueue_sibson(fr_ctx* c, hipStream_t stream = nullptr) {
+  launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, stream ? stream : c->stream);
   return check_launch(c);
 }
 static int enqueue_pullpush(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {
@@ -616,6 +647,7 @@ static int enqueue_atrous(fr_ctx* c, int count, int pos, int nrm, int col, hipSt
 
 static int timed(fr_ctx* c, const std::function<int()>& f, float* ms) {
   hipSetDevice(c->cfg.device);
+  join_recon(c);
   hipEventRecord(c->ev[0], c->stream);
   int rc = f();
   if (rc) return rc;
@@ -667,6 +699,7 @@ int fr_composite_views(fr_ctx* c, const void* views, int nviews, void* out, size
   if (!c || !views || !out || nviews < 1) return FR_E_INVALID;
   const size_t need = (size_t)nviews * c->W * c->H * sizeof(f4);
   if (out_bytes < need) return fail(c, FR_E_INVALID, "fr_composite_views: output smaller than nviews * W * H * 16");
+  join_recon(c);
   hipSetDevice(c->cfg.device);
   launch_composite((const f4*)views, nviews, c->W, c->H, (f4*)out, c->stream);
   int rc = check_launch(c);
@@ -715,28 +748,29 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
   }
   if (t) hipEventRecord(ev[4], c->stream);
   if (recon) {
-    // two independent chains read the shading: JFA -> Sibson, and pull-push -> A-Trous (atFS binds
-    // the JFA texture but never reads it, FR/shader/atFS.glsl:40-90); the second runs on stream2
-    hipEventRecord(ev[11], c->stream);
-    hipStreamWaitEvent(c->stream2, ev[11], 0);
+    // The reconstruction of this frame's shading runs on its own streams, so the next frame's trace
+    // half (on `stream`) overlaps it. Two independent chains read the shading: JFA -> Sibson
+    // (stream3) and pull-push -> A-Trous (stream2; atFS binds the JFA texture but never reads it,
+    // FR/shader/atFS.glsl:40-90). Both resolve their inputs now, at this frame's parity.
+    hipEventRecord(ev[16], c->stream);
+    hipStreamWaitEvent(c->stream3, ev[16], 0);
+    hipStreamWaitEvent(c->stream2, ev[16], 0);
+    if (t) hipEventRecord(ev[20], c->stream3);
+    if ((rc = enqueue_jfa(c, FR_BUF_SHADING, c->stream3))) return rc;
+    if (t) hipEventRecord(ev[21], c->stream3);
+    if ((rc = enqueue_sibson(c, c->stream3))) return rc;
+    if (t) hipEventRecord(ev[22], c->stream3);
     if (t) hipEventRecord(ev[13], c->stream2);
     if ((rc = enqueue_pullpush(c, FR_BUF_SHADING, c->stream2))) return rc;
     if (t) hipEventRecord(ev[14], c->stream2);
     if ((rc = enqueue_atrous(c, c->cfg.atrous_iterations, FR_BUF_POSITION, FR_BUF_NORMAL, FR_BUF_PULLPUSH,
                              c->stream2))) return rc;
     if (t) hipEventRecord(ev[15], c->stream2);
-    hipEventRecord(ev[12], c->stream2);
-    if ((rc = enqueue_jfa(c, FR_BUF_SHADING))) return rc;
-    if (t) hipEventRecord(ev[5], c->stream);
-    if ((rc = enqueue_sibson(c))) return rc;
-    if (t) hipEventRecord(ev[6], c->stream);
-    hipStreamWaitEvent(c->stream, ev[12], 0);  // join: the next launch on the context stream sees both
-    if (t) hipEventRecord(ev[7], c->stream);
-  } else if (t) {
-    for (int i = 5; i <= 7; i++) hipEventRecord(ev[i], c->stream);
-    hipEventRecord(ev[13], c->stream);
-    hipEventRecord(ev[14], c->stream);
-    hipEventRecord(ev[15], c->stream);
+    hipEventRecord(ev[17], c->stream2);
+    hipStreamWaitEvent(c->stream3, ev[17], 0);
+    hipEventRecord(ev[18 + c->par], c->stream3);  // this parity's buffers are free again after this
+    c->recon_pending[c->par] = true;
+    if (t) join_recon(c);
   }
   if (t) {
     hipEventRecord(ev[8], c->stream);
@@ -746,10 +780,10 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     t->sampling_ms = elapsed(ev[1], ev[2]);
     t->optimize_ms = elapsed(ev[2], ev[3]);
     t->shading_ms = elapsed(ev[3], ev[4]);
-    t->jfa_ms = elapsed(ev[4], ev[5]);
-    t->sibson_ms = elapsed(ev[5], ev[6]);
-    t->pullpush_ms = elapsed(ev[13], ev[14]);
-    t->atrous_ms = elapsed(ev[14], ev[15]);
+    t->jfa_ms = recon ? elapsed(ev[20], ev[21]) : 0.0f;
+    t->sibson_ms = recon ? elapsed(ev[21], ev[22]) : 0.0f;
+    t->pullpush_ms = recon ? elapsed(ev[13], ev[14]) : 0.0f;
+    t->atrous_ms = recon ? elapsed(ev[14], ev[15]) : 0.0f;
     t->total_ms = elapsed(ev[0], ev[8]);
     t->shade_paths_ms = elapsed(ev[9], ev[10]);
     hipMemcpy(&t->ray_count, c->ray_count, 4, hipMemcpyDeviceToHost);
@@ -786,6 +820,7 @@ static int shard_io(fr_ctx* c, int id, int rank, void* slab, size_t bytes, bool 
   if (!c || !slab) return FR_E_INVALID;
   if (c->U.shard_count <= 1) return fail(c, FR_E_STATE, "fr_shard_*: call fr_set_shard with count > 1 first");
   if (rank < 0 || rank >= c->U.shard_count) return fail(c, FR_E_INVALID, "fr_shard_unpack: bad source rank");
+  join_recon(c);
   int p;
   if (resolve(c, id, &p)) return fail(c, FR_E_INVALID, "fr_shard_*: buffer is not an RGBA32F image");
   size_t texels = 0;
@@ -808,12 +843,14 @@ int fr_shard_unpack(fr_ctx* c, int id, int src_rank, const void* slab, size_t by
 
 int fr_synchronize(fr_ctx* c) {
   if (!c) return FR_E_INVALID;
+  join_recon(c);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FR_OK;
 }
 
 int fr_ray_count(fr_ctx* c, uint32_t* n) {
   if (!c || !n) return FR_E_INVALID;
+  join_recon(c);
   HIP_TRY(c, hipMemcpyAsync(n, c->ray_count, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FR_OK;
@@ -822,10 +859,11 @@ int fr_ray_count(fr_ctx* c, uint32_t* n) {
 int fr_gaze_target(fr_ctx* c, float xyz[3]) {
   // gaze_target[0] = position_buffer[make_uint2(gaze)] (samplingStep.cu:184)
   if (!c || !xyz) return FR_E_INVALID;
+  join_recon(c);
   uint32_t gx = f2u_sat(c->U.gaze.x), gy = f2u_sat(c->U.gaze.y);
   if (gx >= (uint32_t)c->W || gy >= (uint32_t)c->H) return fail(c, FR_E_STATE, "gaze outside the screen");
   f4 v;
-  HIP_TRY(c, hipMemcpyAsync(&v, c->img[P_POSITION] + (size_t)gy * c->W + gx, sizeof(f4), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(&v, c->img[P_pos(c)] + (size_t)gy * c->W + gx, sizeof(f4), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   xyz[0] = v.x; xyz[1] = v.y; xyz[2] = v.z;
   return FR_OK;
@@ -833,6 +871,7 @@ int fr_gaze_target(fr_ctx* c, float xyz[3]) {
 
 int fr_get_buffer(fr_ctx* c, int id, fr_buffer_view* v) {
   if (!c || !v) return FR_E_INVALID;
+  join_recon(c);  // later work on the context stream is ordered after the reconstruction
   const size_t N = (size_t)c->W * c->H;
   if (id == FR_BUF_THREAD) {
     *v = fr_buffer_view{c->active, (int)N, 1, N * 4, N * 4, FR_FMT_U32};

@@ -202,8 +202,13 @@ int fr_composite_views(fr_ctx* ctx, const void* views, int nviews, void* out, si
  * (x, H - y) from the next launch on (also replaced by fr_set_camera's gaze). */
 int fr_set_gaze(fr_ctx* ctx, float x, float y);
 
-/* The whole main.cpp loop body (update -> 0 -> 1 -> 2 -> 3 -> JFA -> SI -> PPI -> AT), enqueued on the
- * context stream. timing may be NULL (no host synchronisation then; call fr_synchronize). */
+/* The whole main.cpp loop body (update -> 0 -> 1 -> 2 -> 3 -> JFA -> SI -> PPI -> AT). With timing == NULL
+ * nothing is synchronised and consecutive frames pipeline: frame N's reconstruction (JFA -> Sibson and
+ * pull-push -> A-Trous, on two internal streams) runs while frame N+1's trace half runs on the context
+ * stream; POSITION / NORMAL / SHADING alternate between two buffers by frame parity for this. Every
+ * other call (stage launches, buffer access, fr_synchronize) first orders itself after the pending
+ * reconstruction, so results are those of the sequential loop. With timing != NULL the frame is
+ * synchronised and per-stage HIP-event times are returned. */
 int fr_frame(fr_ctx* ctx, fr_frame_timing* timing);
 int fr_trace_frame(fr_ctx* ctx, fr_frame_timing* timing);        /* update -> entries 0..3 only */
 int fr_reconstruct_frame(fr_ctx* ctx, fr_frame_timing* timing);  /* JFA -> SI -> PPI -> AT only */

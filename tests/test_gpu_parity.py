@@ -213,18 +213,20 @@ def test_golden_vectors_on_gpu(fovrt_mod):
 # ---------------------------------------------------------------------------------------------
 # Whole frame: fr_frame == the reference's stage-by-stage call sequence; full-size properties
 # ---------------------------------------------------------------------------------------------
-def test_frame_driver_equals_stage_calls(fovrt_mod):
+@pytest.mark.parametrize("timing", [True, False])  # False: frames pipelined (reconstruction || next trace)
+def test_frame_driver_equals_stage_calls(fovrt_mod, timing):
     W, H = 128, 128
     a = make_tracer(fovrt_mod, W, H, scene=1, mask=1, spp=4, dmd=3)
     b = make_tracer(fovrt_mod, W, H, scene=1, mask=1, spp=4, dmd=3)
-    for _ in range(3):
-        a.frame(timing=True)
+    for _ in range(4):
+        a.frame(timing=timing)
         b.geometry_launch(); b.sampling_launch(); b.optimize_launch(); b.shading_launch()
         fovrt_mod.JumpFlooding(b).render(TN.SHADING)
         fovrt_mod.SibsonInterpolation(b).render()
         fovrt_mod.PullPushInterpolation(b).render(TN.SHADING)
         fovrt_mod.ATrous(b).render(1, TN.POSITION, TN.NORMAL, TN.PULLPUSH)
-    for tid in (TN.SHADING, TN.JFA_COLOR, TN.SIBSON, TN.PULLPUSH, TN.ATROUS, TN.HISTORY_CACHE):
+    for tid in (TN.SHADING, TN.JFA_COLOR, TN.SIBSON, TN.PULLPUSH, TN.ATROUS, TN.HISTORY_CACHE, TN.POSITION,
+                TN.NORMAL, TN.DEPTH_CACHE):
         assert equal_nan(a.read(tid), b.read(tid)), tid
 
 
