@@ -26,7 +26,8 @@ void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*
 size_t shade_counter_words();
 void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
 void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
-                     const f4*, f4*, uint8_t*, const uint8_t*, unsigned long long*, uint32_t*, int, hipStream_t);
+                     const f4*, f4*, uint8_t*, const uint8_t*, unsigned long long*, uint32_t*, int, uint8_t*, bool,
+                     hipStream_t);
 void launch_mask_words(const uint8_t*, const uint8_t*, int, int, unsigned long long*, uint32_t*, hipStream_t);
 void launch_compaction(int, int, const unsigned long long*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                        uint32_t*, hipStream_t);
@@ -85,6 +86,9 @@ struct fr_ctx {
   int atrous_out = P_ATROUS_A;
   uint8_t* mask = nullptr;
   uint8_t* gclass = nullptr;
+  uint8_t* lp_cache = nullptr;  // log-polar mask for (lp_gaze, lp_mode); recomputed when either changes
+  f2 lp_gaze{-1e30f, -1e30f};
+  int lp_mode = -1;
   unsigned long long* words = nullptr;
   uint32_t* counts = nullptr;
   uint32_t* offsets = nullptr;  // per (class, block) local prefix
@@ -416,7 +420,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   c->pp_S = pp_size(c->W, c->H);
   const size_t atlas = (size_t)c->pp_S * (c->pp_S + c->pp_S / 2);
   if (compaction_tiles(c->W, c->H) > 1024) { c->err = "screen too large for the compaction scan"; return bail(FR_E_UNSUPPORTED); }
-  if (dalloc(&c->mask, N) != hipSuccess || dalloc(&c->gclass, N) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
+  if (dalloc(&c->mask, N) != hipSuccess || dalloc(&c->gclass, N) != hipSuccess || dalloc(&c->lp_cache, N) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
       dalloc(&c->counts, 4 * nblocks) != hipSuccess || dalloc(&c->offsets, 4 * nblocks) != hipSuccess ||
       dalloc(&c->tiles, 1024) != hipSuccess || dalloc(&c->ray_count, 4) != hipSuccess ||
       dalloc(&c->active, N) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
@@ -467,7 +471,7 @@ int fr_destroy(fr_ctx* c) {
   for (auto p : c->d_tex) fr(p);
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
-  fr(c->mask); fr(c->gclass); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->jfa_a); fr(c->jfa_b);
+  fr(c->mask); fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->jfa_a); fr(c->jfa_b);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -547,9 +551,13 @@ static int enqueue_geometry(fr_ctx* c) {
 
 static int enqueue_sampling(fr_ctx* c) {
   c->mask_dirty = false;
+  const bool lp = c->U.mask_mode == FR_MASK_LOGPOLAR || c->U.mask_mode == FR_MASK_LOGPOLAR_SIGNED;
+  const bool lp_refresh = lp && (c->lp_mode != c->U.mask_mode || c->lp_gaze.x != c->U.gaze.x ||
+                                 c->lp_gaze.y != c->U.gaze.y);
+  if (lp_refresh) { c->lp_mode = c->U.mask_mode; c->lp_gaze = c->U.gaze; }
   launch_sampling(c->U, c->dsc, c->img[P_pos(c)], c->img[c->depth_cur], c->img[c->depth_cache], c->img[P_WEIGHT],
                   c->img[P_nrm(c)], c->img[P_DIFFUSE], c->img[P_EXTRA], c->mask, c->gclass, c->words, c->counts,
-                  c->cfg.write_extra, c->stream);
+                  c->cfg.write_extra, c->lp_cache, lp_refresh, c->stream);
   c->compacted = false;
   return check_launch(c);
 }

@@ -125,3 +125,40 @@ def test_oracle_matches_golden(oracle, name):
         assert [oracle.tea16(int(a), int(b)) for a, b in g["tea_in"]] == list(g["tea_out"])
         assert np.array_equal(oracle.rnd_seq(int(g["rnd_seed"]), len(g["rnd_out"])), g["rnd_out"])
         assert np.allclose(oracle.tonemap(g["tm_in"]), g["tm_out"], rtol=1e-6, atol=0)
+
+
+def _sqrt_le_bound(d):
+    """numpy mirror of k_image.hip sqrt_le_bound: the largest float32 x with sqrtf(x) <= d."""
+    f32 = np.float32
+    c = f32(d) * f32(d)
+    while c > 0 and np.sqrt(c) > d:
+        c = np.nextafter(c, f32(0))
+    while True:
+        n = np.nextafter(c, f32(np.inf))
+        if not np.sqrt(n) <= d:
+            return c
+        c = n
+
+
+def test_sqrt_free_disc_test_is_exact():
+    """Sibson's disc test 'sqrtf(r2) > d' is replaced by 'r2 > sqrt_le_bound(d)' (k_image.hip):
+    equivalent for every float32 r2 >= 0 because sqrtf is correctly rounded and monotone. Checked
+    here on the ulps around d*d and on random values."""
+    rs = np.random.RandomState(3)
+    ds = np.concatenate([rs.rand(300).astype(np.float32) * np.float32(0.01),
+                         np.float32([0.0, 1e-20, 2.6e-4, 1.0, 3.0])])
+    for d in ds:
+        d = np.float32(d)
+        b = _sqrt_le_bound(d)
+        c = np.float32(d * d)
+        probe = [c, b] + [np.nextafter(c, np.float32(np.inf)) for _ in range(1)]
+        x = c
+        for _ in range(8):
+            x = np.nextafter(x, np.float32(0)); probe.append(x)
+        x = c
+        for _ in range(8):
+            x = np.nextafter(x, np.float32(np.inf)); probe.append(x)
+        probe += list((rs.rand(50) * 4 * float(c) + 1e-30).astype(np.float32))
+        for r2 in probe:
+            r2 = np.float32(r2)
+            assert (np.sqrt(r2) > d) == (r2 > b), (d, r2, b)

@@ -361,3 +361,17 @@ def test_composite_views_side_by_side(fovrt_mod):
     img = out.cpu().numpy().reshape(H, 2 * W, 4)
     assert equal_nan(img[:, :W], eyes[0].read(TN.ATROUS)) and equal_nan(img[:, W:], eyes[1].read(TN.ATROUS))
     assert not equal_nan(img[:, :W], img[:, W:])  # two different eyes
+
+
+def test_logpolar_mask_cache_follows_the_gaze(fovrt_mod):
+    """The log-polar sampling mask is cached between frames and recomputed when the gaze moves."""
+    W, H = 160, 96
+    t = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=1, dmd=1)
+    for gaze_window in (None, None, (40.0, 30.0), (40.0, 30.0), (150.0, 90.0)):
+        if gaze_window is not None:
+            t.set_gaze(*gaze_window)
+            g = (np.float32(gaze_window[0]), np.float32(H) - np.float32(gaze_window[1]))
+        else:
+            g = (W // 2, H - H // 2)
+        t.frame(timing=False)
+        assert np.array_equal(t.read(TN.MASK), logpolar_mask_np(W, H, g[0], g[1], signed=True)), gaze_window
