@@ -141,6 +141,18 @@ def gather_slabs(dist, group, slab, gather_list, dst):
     dist.gather(slab, gather_list=gather_list, dst=dst, group=group)
 
 
+def allgather_slabs(dist, group, slab, out_list):
+    """All-gather of every rank's packed tiles (the moving-camera history exchange), staged through
+    host memory over gloo like gather_slabs."""
+    if dist.get_backend() == "gloo" and slab.is_cuda:
+        hl = [t.cpu() for t in out_list]
+        dist.all_gather(hl, slab.cpu(), group=group)
+        for t, h in zip(out_list, hl):
+            t.copy_(h)
+        return
+    dist.all_gather(out_list, slab, group=group)
+
+
 def load_traffic(kernels, config):
     """HBM bytes per launch of `kernels` from the newest profiles/*_pmc_traffic.json recorded on the
     same workload (scripts/profile.sh), else None."""
@@ -182,6 +194,10 @@ def main():
     ap.add_argument("--composite", action="store_true",
                     help="every frame, gather the views' reconstructed images to rank 0 over RCCL and compose them "
                          "side by side (the final composite of the stereo configuration)")
+    ap.add_argument("--pan", type=float, default=0.0,
+                    help="per-frame step of the camera's look-at target in scene units (0: static camera). A "
+                         "moving camera makes the history reprojection read across tiles; tile-sharded views "
+                         "then all-gather HISTORY_CACHE every frame")
     args = ap.parse_args()
     args.mask = fovrt.MASKS[args.mask]
     scene = fovrt.SCENES[args.scene]
@@ -238,6 +254,9 @@ def main():
             gather_list = [torch.empty_like(slab) for _ in range(G)]
         nbytes = n_tex * 16
         root = view * G
+        if args.pan:
+            hist_slab = torch.empty_like(slab)
+            hist_list = [torch.empty_like(slab) for _ in range(G)]
 
     comp_img = comp_list = comp_out = None
     if roots_group is not None and vrank == 0:
@@ -260,14 +279,39 @@ def main():
     def step(timing):
         """One frame of the view: the whole chain on one rank, or trace -> pack -> gather -> (root)
         unpack + reconstruct when the view is tile-sharded; then the optional final composite."""
+        if args.pan:
+            move_camera()
         tm = view_frame(timing)
         composite()
         return tm
+
+    step_dir = np.array([1.0, 0.5, 0.0], np.float32)
+    step_dir *= np.float32(args.pan) / np.linalg.norm(step_dir)
+
+    def move_camera():
+        """Camera path of the moving-camera runs: the eye stays, the look-at target moves a fixed step per
+        frame (setPrevState first, so frame N reprojects into frame N-1 as FR/main.cpp:357 does)."""
+        cam.setPrevState()
+        cam.lookAt(np.asarray(cam.target) + step_dir)
+        tracer.update_optix_variables(cam)
+
+    def exchange_history():
+        """Reprojection reads the previous frame's history anywhere on the screen, so with a moving camera
+        every rank of a view needs the others' tiles of HISTORY_CACHE before its next trace."""
+        tracer.shard_pack(fovrt.TextureName.HISTORY_CACHE, hist_slab.data_ptr(), nbytes)
+        allgather_slabs(dist, groups[view], hist_slab, hist_list)
+        sync()
+        for r in range(G):
+            if r != vrank:
+                tracer.shard_unpack(fovrt.TextureName.HISTORY_CACHE, r, hist_list[r].data_ptr(), nbytes)
 
     def view_frame(timing):
         if G == 1:
             return tracer.frame(timing=timing)
         tm = tracer.trace_frame(timing=timing)
+        if args.pan:
+            exchange_history()
+        sync()  # the previous frame's gather of `slab` has finished on torch's stream
         tracer.shard_pack(fovrt.TextureName.SHADING, slab.data_ptr(), nbytes)
         gather_slabs(dist, groups[view], slab, gather_list, root)
         if vrank == 0:
@@ -323,7 +367,9 @@ def main():
     rho = float(np.mean(ray_counts)) * G / (W * H)
     L = jfa_passes(W, H)
     sb = stage_bytes(W, H, rho, args.spp, L)
-    stage_table = {k: {"ms": round(avg[k], 4), "GB/s": round(sb[k] / (avg[k] * 1e-3) / 1e9, 1)} for k in sb}
+    # (a non-compositing rank of a tile-sharded view runs no reconstruction: its image stages are 0 ms)
+    stage_table = {k: {"ms": round(avg[k], 4),
+                       "GB/s": round(sb[k] / (avg[k] * 1e-3) / 1e9, 1) if avg[k] > 0 else None} for k in sb}
     # the dominant stage is entry 3 (shading_launch): k_shade_paths (path-trace megakernel) +
     # k_shade_resolve + k_carry_history; its algorithmic bytes are SURVEY §8(d)'s (56 + 4 rho) B/px.
     dominant = max(sb, key=lambda k: avg[k])
@@ -351,7 +397,7 @@ def main():
                                "JFA + Sibson + pull-push + A-Trous",
                    "scene": args.scene, "width": W, "height": H, "spp": args.spp, "diffuse_max_depth": args.dmd,
                    "mask_mode": args.mask, "foveal_density": round(rho, 5), "views": views,
-                   "composite": bool(args.composite and views > 1),
+                   "composite": bool(args.composite and views > 1), "camera_step": args.pan,
                    "parallelism": (f"views x{world} (one view per GPU)" if G == 1 else
                                    f"{views} view(s) x {G}-way {args.tile}px tile sharding, RCCL gather to the "
                                    f"view's first rank"),

@@ -16,6 +16,12 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def fovrt_mod():
+    # torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's): load it before libfovrt so the
+    # process has the one HIP runtime torch was built against (the tests use torch device memory)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     import fovrt
     fovrt.load_library()
     return fovrt

@@ -63,14 +63,16 @@ def _tile_worker(rank, world, views, port, q):
     slab = torch.full((8,), float(rank))
     gl = [torch.empty_like(slab) for _ in range(g)] if vrank == 0 else None
     bench.gather_slabs(dist, groups[view], slab, gl, view * g)
-    q.put((rank, view, vrank, g, None if gl is None else [float(t[0]) for t in gl]))
+    al = [torch.empty_like(slab) for _ in range(g)]  # the moving-camera history exchange
+    bench.allgather_slabs(dist, groups[view], slab, al)
+    q.put((rank, view, vrank, g, None if gl is None else [float(t[0]) for t in gl], [float(t[0]) for t in al]))
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_tile_gather_groups_gloo_world4():
     """4 ranks, 2 views (the stereo layout of BASELINE configs[4] at half size): each view's 2 ranks
-    gather their slabs to the view's first rank."""
+    gather their slabs to the view's first rank, and all-gather them within the view."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -81,8 +83,9 @@ def test_tile_gather_groups_gloo_world4():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert out[0] == [0, 0, 2, [0.0, 1.0]] and out[2] == [1, 0, 2, [2.0, 3.0]]
+    assert out[0][:4] == [0, 0, 2, [0.0, 1.0]] and out[2][:4] == [1, 0, 2, [2.0, 3.0]]
     assert out[1][3] is None and out[3][3] is None
+    assert out[0][4] == out[1][4] == [0.0, 1.0] and out[2][4] == out[3][4] == [2.0, 3.0]
 
 
 def test_view_layout():

@@ -320,6 +320,60 @@ def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile):
     assert np.array_equal(masks, full.read(TN.MASK))  # the ranks' masks partition the full mask
 
 
+@pytest.mark.parametrize("scene,mask", [(0, 0), (0, 4), (1, 4)])
+def test_tile_shards_moving_camera_with_history_exchange(fovrt_mod, scene, mask):
+    """Moving camera: reprojection reads the previous frame's history at other ranks' tiles, so every
+    rank all-gathers HISTORY_CACHE after its trace half (bench.py exchange_history). With that exchange
+    the composite equals the single-context frame bit for bit; without it, it does not."""
+    import torch
+    W, H, nranks, tile = 160, 112, 2, 8
+    mk = lambda: make_tracer(fovrt_mod, W, H, scene=scene, mask=mask, spp=2, dmd=2)
+    full, ranks, stale = mk(), [mk() for _ in range(nranks)], [mk() for _ in range(nranks)]
+    for group in (ranks, stale):
+        for r, t in enumerate(group):
+            t.set_shard(r, nranks, tile)
+    n = ranks[0].shard_texels()
+    slabs = [torch.zeros(n * 4, dtype=torch.float32, device="cuda") for _ in range(nranks)]
+    cam = fovrt_mod.Camera.preset(scene, W, H)
+    diverged, cross = False, 0
+    for f in range(5):
+        cam.setPrevState()
+        cam.lookAt(np.asarray(cam.target) + np.array([0.03, 0.02, 0.0], np.float32))  # pan: the eye stays
+        for t in [full] + ranks + stale:
+            t.update_optix_variables(cam)
+        full.frame(timing=False)
+        for group, exchange in ((ranks, True), (stale, False)):
+            for t in group:
+                t.trace_frame(timing=False)
+            if exchange:  # all-gather of HISTORY_CACHE (the buffer the next frame reprojects from)
+                for r, t in enumerate(group):
+                    t.shard_pack(TN.HISTORY_CACHE, slabs[r].data_ptr(), n * 16)
+                for r, t in enumerate(group):
+                    for s in range(nranks):
+                        if s != r:
+                            t.shard_unpack(TN.HISTORY_CACHE, s, slabs[s].data_ptr(), n * 16)
+            for r, t in enumerate(group):
+                t.shard_pack(TN.SHADING, slabs[r].data_ptr(), n * 16)
+            for r in range(1, nranks):
+                group[0].shard_unpack(TN.SHADING, r, slabs[r].data_ptr(), n * 16)
+            group[0].reconstruct_frame(timing=False)
+        for tid in (TN.SHADING, TN.ATROUS):
+            assert equal_nan(ranks[0].read(tid), full.read(tid)), (f, tid)
+        assert equal_nan(ranks[1].read(TN.HISTORY_CACHE), full.read(TN.HISTORY_CACHE)), f
+        # valid reprojections whose source texel lies in a tile of the other rank
+        wgt = full.read(TN.WEIGHT)
+        ys, xs = np.nonzero(wgt[..., 2] > 0)
+        qx = np.floor(wgt[ys, xs, 0] + np.float32(0.5)).astype(np.int64)
+        qy = np.floor(wgt[ys, xs, 1] + np.float32(0.5)).astype(np.int64)
+        tiles_x = (W + tile - 1) // tile
+        owner = lambda x, y: ((y // tile) * tiles_x + x // tile) % nranks
+        cross += int(np.count_nonzero(owner(xs, ys) != owner(qx, qy)))
+        diverged |= not equal_nan(stale[0].read(TN.SHADING), full.read(TN.SHADING))
+    print("valid:", len(xs), "cross-tile:", cross, "stale diverged:", diverged)
+    assert cross > 0  # the camera motion makes ranks read each other's history
+    assert diverged  # ... and the exchange is what keeps the tiles exact
+
+
 # ---------------------------------------------------------------------------------------------
 # LogPolarTransform (FR/Log_Polar_Transform.cpp:40-106) and the gaze input (FR/gui.cpp:48-66)
 # ---------------------------------------------------------------------------------------------
