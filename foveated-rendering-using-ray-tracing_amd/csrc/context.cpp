@@ -38,6 +38,11 @@ void launch_composite(const f4*, int, int, int, f4*, hipStream_t);
 void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
+#ifdef FR_STAMPS
+void launch_trace_queries(const DevScene&, const f4*, uint32_t, f4*, uint32_t*, hipStream_t, int);
+void diag_record_queries(f4*, uint32_t, hipStream_t);
+uint32_t diag_recorded_queries(hipStream_t);
+#endif
 void launch_pullpush(const f4*, f4*, f4*, f4*, f4*, int, int, hipStream_t);
 void launch_atrous(const f4*, const f4*, const f4*, f4*, int, int, float, float, float, float, hipStream_t);
 int pp_size(int W, int H);
@@ -919,6 +924,75 @@ int fr_write_buffer(fr_ctx* c, int id, const void* host, size_t bytes) {
   }
   return FR_OK;
 }
+
+#ifdef FR_STAMPS
+// Diagnostic probe (libfovrt_diag.so only, not part of the ABI): records every query of one shading
+// launch (geometry / sampling / optimize must have run), then traces the recorded stream with
+// k_trace_queries. out = {queries, best ms of 5 runs, shadow queries, ms of the stream partitioned by
+// kind, ms of its closest-hit part (specialised kernel), ms of its shadow part (specialised kernel)}.
+extern "C" int fr_diag_trace_queries(fr_ctx* c, float* out) {
+  if (!c || !out) return FR_E_INVALID;
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  const uint32_t cap = 48u << 20;
+  f4 *rec = nullptr, *hits = nullptr;
+  uint32_t* ctr = nullptr;
+  HIP_TRY(c, hipMalloc(&rec, (size_t)cap * 32));
+  HIP_TRY(c, hipMalloc(&hits, (size_t)cap * 16));
+  HIP_TRY(c, hipMalloc(&ctr, 4));
+  diag_record_queries(rec, cap, c->stream);
+  int rc = enqueue_shading(c);
+  if (rc) return rc;
+  uint32_t n = std::min(diag_recorded_queries(c->stream), cap);
+  diag_record_queries(nullptr, 0, c->stream);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  // best of 5 runs of fn() on the context stream
+  auto timeit = [&](auto fn) {
+    float best = 1e30f;
+    for (int r = 0; r < 5; r++) {
+      hipEventRecord(a, c->stream);
+      fn();
+      hipEventRecord(b, c->stream);
+      hipStreamSynchronize(c->stream);
+      float ms = 0;
+      hipEventElapsedTime(&ms, a, b);
+      best = std::min(best, ms);
+    }
+    return best;
+  };
+  const float t_mixed = timeit([&] { launch_trace_queries(c->dsc, rec, n, hits, ctr, c->stream, 0); });
+  // the same stream partitioned by kind (closest-hit first, then shadow; order within a kind kept)
+  std::vector<f4> d((size_t)n * 2), part;
+  HIP_TRY(c, hipMemcpy(d.data(), rec, (size_t)n * 32, hipMemcpyDeviceToHost));
+  part.reserve(d.size());
+  for (int pass = 0; pass < 2; pass++)
+    for (uint32_t i = 0; i < n; i++)
+      if ((d[2 * (size_t)i + 1].w != 0.0f) == (pass == 1)) { part.push_back(d[2 * (size_t)i]); part.push_back(d[2 * (size_t)i + 1]); }
+  size_t shadow = 0;
+  for (uint32_t i = 0; i < n; i++) shadow += d[2 * (size_t)i + 1].w != 0.0f;
+  const uint32_t nc = n - (uint32_t)shadow;
+  HIP_TRY(c, hipMemcpy(rec, part.data(), (size_t)n * 32, hipMemcpyHostToDevice));
+  const float t_sorted = timeit([&] { launch_trace_queries(c->dsc, rec, n, hits, ctr, c->stream, 0); });
+  const float t_closest = timeit([&] { launch_trace_queries(c->dsc, rec, nc, hits, ctr, c->stream, 1); });
+  const float t_shadow =
+      timeit([&] { launch_trace_queries(c->dsc, rec + 2 * (size_t)nc, (uint32_t)shadow, hits, ctr, c->stream, 2); });
+  out[3] = t_sorted;
+  out[4] = t_closest;
+  out[5] = t_shadow;
+  const float best = t_mixed;
+  out[0] = (float)n;
+  out[1] = best;
+  out[2] = (float)shadow;
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  hipFree(rec);
+  hipFree(hits);
+  hipFree(ctr);
+  return check_launch(c);
+}
+#endif
 
 int fr_get_stats(fr_ctx* c, fr_stats* s) {
   if (!c || !s) return FR_E_INVALID;
