@@ -56,6 +56,17 @@ struct DevMaterial {
 #define FR_MAX_TEXTURES 8
 #define FR_MAX_MATERIALS 8
 
+// Packed fp32 (v_pk_add_f32 / v_pk_mul_f32, two values per lane). Every element goes through
+// exactly the operations of its scalar form, in the same order, so results are bit-identical.
+typedef float v2f __attribute__((ext_vector_type(2)));
+FR_HD v2f v2(float a, float b) {
+  v2f r;
+  r.x = a;
+  r.y = b;
+  return r;
+}
+FR_HD v2f v2s(float a) { return v2(a, a); }
+
 struct DevScene {
   const BvhNode* nodes;
   const TriGeo* tri_geo;
