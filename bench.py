@@ -194,6 +194,8 @@ def main():
     ap.add_argument("--composite", action="store_true",
                     help="every frame, gather the views' reconstructed images to rank 0 over RCCL and compose them "
                          "side by side (the final composite of the stereo configuration)")
+    ap.add_argument("--bvh", default="host", choices=["host", "gpu"],
+                    help="BVH builder: host binned SAH (default) or the GPU LBVH (k_bvh.hip)")
     ap.add_argument("--pan", type=float, default=0.0,
                     help="per-frame step of the camera's look-at target in scene units (0: static camera). A "
                          "moving camera makes the history reprojection read across tiles; tile-sharded views "
@@ -235,7 +237,8 @@ def main():
     roots_group = (dist.new_group([v * (world // views) for v in range(views)])
                    if dist is not None and args.composite and views > 1 else None)
     cfg = fovrt.Config(width=W, height=H, scene=scene, mask_mode=args.mask, spp=args.spp, diffuse_max_depth=args.dmd,
-                       refraction_max_depth=args.refraction_max_depth, device=device)
+                       refraction_max_depth=args.refraction_max_depth, device=device,
+                       bvh_builder=1 if args.bvh == "gpu" else 0)
     tracer = fovrt.PathTracer(cfg)
     tracer.initialize()
     cam = fovrt.Camera.preset(scene, W, H)
@@ -428,6 +431,10 @@ def main():
         result["roofline"]["traffic"] = int(traffic)
         result["roofline"]["traffic_source"] = src
         result["roofline"]["measured_hbm_GBs"] = round(traffic / (avg[dominant] * 1e-3) / 1e9, 1)
+    # the GPU BVH builder on this scene (after every measurement: it replaces the BVH)
+    builds = sorted(tracer.rebuild_bvh() for _ in range(3))
+    result["bvh"] = {"builder": args.bvh, "gpu_rebuild_ms": round(builds[1], 3),
+                     "triangles": int(tracer.scene_arrays()["pos"].shape[0])}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             arrays = tracer.scene_arrays()

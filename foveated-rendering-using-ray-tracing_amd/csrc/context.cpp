@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include <chrono>
 #include "../../include/fovrt.h"
 #include "fr_device.h"
 #include "scene.h"
@@ -38,6 +39,7 @@ void launch_composite(const f4*, int, int, int, f4*, hipStream_t);
 void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
+bool gpu_build_bvh(const f3*, int, BvhNode**, TriGeo**, int32_t**, int*, int*, hipStream_t, std::string&);
 #ifdef FR_STAMPS
 void launch_trace_queries(const DevScene&, const f4*, uint32_t, f4*, uint32_t*, hipStream_t, int);
 void diag_record_queries(f4*, uint32_t, hipStream_t);
@@ -77,6 +79,7 @@ struct fr_ctx {
   Bvh bvh;
   // device scene
   BvhNode* d_nodes = nullptr;
+  f3* d_pos = nullptr;  // world-space vertices, 3 per triangle (the GPU builder's input)
   TriGeo* d_tri = nullptr;
   int32_t* d_prim = nullptr;
   TriShade* d_shade = nullptr;
@@ -334,6 +337,41 @@ int fr_camera_uniforms(const fr_camera_pose* cur, const fr_camera_pose* prev, in
   return FR_OK;
 }
 
+// GPU build over c->d_pos (k_bvh.hip): replaces the device BVH arrays and mirrors them into
+// c->bvh (fr_scene_export).
+static int gpu_rebuild(fr_ctx* c) {
+  const int nt = c->scene.num_tris();
+  BvhNode* nodes = nullptr;
+  TriGeo* tri = nullptr;
+  int32_t* prim = nullptr;
+  int nn = 0, max_stack = 0;
+  std::string err;
+  if (!gpu_build_bvh(c->d_pos, nt, &nodes, &tri, &prim, &nn, &max_stack, c->stream, err)) {
+    c->err = err;
+    return FR_E_HIP;
+  }
+  if (max_stack > FR_BVH_STACK) {
+    hipFree(nodes); hipFree(tri); hipFree(prim);
+    c->err = "GPU BVH needs a traversal stack deeper than FR_BVH_STACK";
+    return FR_E_UNSUPPORTED;
+  }
+  if (c->d_nodes) hipFree(c->d_nodes);
+  if (c->d_tri) hipFree(c->d_tri);
+  if (c->d_prim) hipFree(c->d_prim);
+  c->d_nodes = nodes; c->d_tri = tri; c->d_prim = prim;
+  c->dsc.nodes = nodes; c->dsc.tri_geo = tri; c->dsc.tri_prim = prim;
+  Bvh& b = c->bvh;
+  b.nodes.resize(nn); b.tri_geo.resize(nt); b.tri_prim.resize(nt);
+  b.root_count = 0; b.max_stack = max_stack; b.max_depth = 0;
+  if (hipMemcpy(b.nodes.data(), nodes, (size_t)nn * sizeof(BvhNode), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(b.tri_geo.data(), tri, (size_t)nt * sizeof(TriGeo), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(b.tri_prim.data(), prim, (size_t)nt * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) {
+    c->err = "GPU BVH: readback failed";
+    return FR_E_HIP;
+  }
+  return FR_OK;
+}
+
 int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (!out) return fail(nullptr, FR_E_INVALID, "out is NULL");
   *out = nullptr;
@@ -372,10 +410,13 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     c->err = "scene: " + err;
     return bail(FR_E_IO);
   }
-  build_bvh(c->scene, c->bvh);
-  if (c->bvh.max_stack > FR_BVH_STACK) {
-    c->err = "BVH needs a traversal stack deeper than FR_BVH_STACK";
-    return bail(FR_E_UNSUPPORTED);
+  if (cfg.bvh_builder < 0 || cfg.bvh_builder > 1) { c->err = "bad bvh_builder"; return bail(FR_E_INVALID); }
+  if (cfg.bvh_builder == 0) {
+    build_bvh(c->scene, c->bvh);
+    if (c->bvh.max_stack > FR_BVH_STACK) {
+      c->err = "BVH needs a traversal stack deeper than FR_BVH_STACK";
+      return bail(FR_E_UNSUPPORTED);
+    }
   }
   const HostScene& s = c->scene;
   const int nt = s.num_tris();
@@ -392,10 +433,17 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     if (dalloc((T**)dst, vec.size()) != hipSuccess) return false;
     return hipMemcpy(*dst, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
   };
-  if (!up(&c->d_nodes, c->bvh.nodes) || !up(&c->d_tri, c->bvh.tri_geo) || !up(&c->d_prim, c->bvh.tri_prim) ||
-      !up(&c->d_shade, shade)) {
+  if (!up(&c->d_shade, shade) || !up(&c->d_pos, s.pos)) {
     c->err = "device allocation (scene) failed";
     return bail(FR_E_NOMEM);
+  }
+  if (cfg.bvh_builder == 0) {
+    if (!up(&c->d_nodes, c->bvh.nodes) || !up(&c->d_tri, c->bvh.tri_geo) || !up(&c->d_prim, c->bvh.tri_prim)) {
+      c->err = "device allocation (scene) failed";
+      return bail(FR_E_NOMEM);
+    }
+  } else if (int rc = gpu_rebuild(c)) {
+    return bail(rc);
   }
   DevScene& d = c->dsc;
   memset(&d, 0, sizeof(d));
@@ -472,7 +520,7 @@ int fr_destroy(fr_ctx* c) {
   if (c->stream2) hipStreamSynchronize(c->stream2);
   if (c->stream3) hipStreamSynchronize(c->stream3);
   auto fr = [](void* p) { if (p) hipFree(p); };
-  fr(c->d_nodes); fr(c->d_tri); fr(c->d_prim); fr(c->d_shade);
+  fr(c->d_nodes); fr(c->d_tri); fr(c->d_prim); fr(c->d_shade); fr(c->d_pos);
   for (auto p : c->d_tex) fr(p);
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
@@ -923,6 +971,29 @@ int fr_write_buffer(fr_ctx* c, int id, const void* host, size_t bytes) {
     c->mask_dirty = true;
   }
   return FR_OK;
+}
+
+int fr_rebuild_bvh(fr_ctx* c, float* ms) {
+  if (!c) return FR_E_INVALID;
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = gpu_rebuild(c);
+  if (ms) *ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
+}
+
+static_assert(sizeof(f3) == 3 * sizeof(float), "f3 must be three packed floats");
+int fr_set_positions(fr_ctx* c, const float* xyz, size_t ntris) {
+  if (!c || !xyz) return FR_E_INVALID;
+  if (ntris != (size_t)c->scene.num_tris()) return fail(c, FR_E_INVALID, "fr_set_positions: triangle count differs");
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  memcpy(c->scene.pos.data(), xyz, ntris * 9 * sizeof(float));
+  HIP_TRY(c, hipMemcpy(c->d_pos, xyz, ntris * 9 * sizeof(float), hipMemcpyHostToDevice));
+  return gpu_rebuild(c);
 }
 
 #ifdef FR_STAMPS

@@ -52,7 +52,7 @@ class fr_config(C.Structure):
                 ("spp", C.c_int), ("diffuse_max_depth", C.c_int), ("refraction_max_depth", C.c_int),
                 ("light_power", C.c_float), ("optimize", C.c_int), ("atrous_iterations", C.c_int),
                 ("write_extra", C.c_int), ("device", C.c_int), ("texture_mode", C.c_int), ("detail", C.c_int),
-                ("mesh_mode", C.c_int), ("asset_dir", C.c_char_p)]
+                ("mesh_mode", C.c_int), ("bvh_builder", C.c_int), ("asset_dir", C.c_char_p)]
 
 
 class fr_camera(C.Structure):
@@ -134,6 +134,8 @@ _SIGS = {
     "fr_read_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_write_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_copy_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
+    "fr_rebuild_bvh": [C.c_void_p, C.POINTER(C.c_float)],
+    "fr_set_positions": [C.c_void_p, C.POINTER(C.c_float), C.c_size_t],
     "fr_get_stats": [C.c_void_p, C.POINTER(fr_stats)],
     "fr_reset_stats": [C.c_void_p],
     "fr_scene_export": [C.c_void_p, C.POINTER(fr_scene_arrays)],
@@ -273,6 +275,7 @@ class Config:
     texture_mode: int = 0
     detail: int = 0
     mesh_mode: int = 0  # 0: .obj meshes where present, else procedural; 1: procedural; 2: .obj required
+    bvh_builder: int = 0  # 0: host binned SAH; 1: GPU LBVH (k_bvh.hip)
     asset_dir: str = DEFAULT_ASSET_DIR
 
     def to_c(self) -> fr_config:
@@ -439,6 +442,17 @@ class PathTracer:
         """Side-by-side composite of nviews W x H device images into (nviews W) x H (device pointers)."""
         self._check(_lib.fr_composite_views(self._ctx, C.c_void_p(views_ptr), int(nviews), C.c_void_p(out_ptr),
                                             int(out_bytes)))
+
+    def rebuild_bvh(self) -> float:
+        """Re-indexes the current triangles with the GPU builder; returns its wall time in ms."""
+        return self._launch(_lib.fr_rebuild_bvh)
+
+    def set_positions(self, xyz: np.ndarray):
+        """New world-space vertex positions (ntris x 3 x 3 float32, scene triangle order), then a GPU
+        rebuild of the BVH."""
+        a = np.ascontiguousarray(xyz, dtype=np.float32)
+        n = a.size // 9
+        self._check(_lib.fr_set_positions(self._ctx, a.ctypes.data_as(C.POINTER(C.c_float)), n))
 
     def set_gaze(self, x, y):
         """cursorPosCallback (FR/gui.cpp:48-66): gaze in window coordinates (y down)."""

@@ -67,6 +67,8 @@ typedef struct fr_config {
   int detail;                 /* procedural mesh detail (0 = preset default) */
   int mesh_mode;              /* 0: the reference's .obj meshes where present under asset_dir, procedural
                                * stand-ins otherwise; 1: procedural only; 2: .obj required (FR_E_IO) */
+  int bvh_builder;            /* 0: host binned SAH (default); 1: GPU LBVH (k_bvh.hip), the builder of
+                               * fr_rebuild_bvh / fr_set_positions; both give identical frames */
   const char* asset_dir;      /* directory holding CedarCity.hdr, grid.ppm, bunny/bunny.PPM, ... */
 } fr_config;
 
@@ -227,6 +229,15 @@ int fr_shard_texels(fr_ctx* ctx, size_t* texels);
 int fr_shard_pack(fr_ctx* ctx, int buffer_id, void* device_slab, size_t bytes);
 int fr_shard_unpack(fr_ctx* ctx, int buffer_id, int src_rank, const void* device_slab, size_t bytes);
 
+
+/* GPU BVH builder (the reference's OptiX acceleration rebuild,
+ * FR/PathTracer.cpp:590-602 rtAccelerationCreate(ctx, "Trbvh")). fr_rebuild_bvh re-indexes the
+ * current triangles on the device (LBVH: Morton sort + Karras hierarchy, collapsed into the
+ * engine's four-wide nodes); *ms = its wall time. fr_set_positions replaces the world-space
+ * vertex positions (host array, 9 floats per triangle, the scene's triangle order) and rebuilds;
+ * shading normals, texture coordinates and materials are kept. */
+int fr_rebuild_bvh(fr_ctx* ctx, float* ms);
+int fr_set_positions(fr_ctx* ctx, const float* xyz, size_t ntris);
 /* Buffer access (PathTracer::get_texture, FR/PathTracer.cpp:337-374; rtBufferMap). */
 int fr_get_buffer(fr_ctx* ctx, int id, fr_buffer_view* view);
 int fr_read_buffer(fr_ctx* ctx, int id, void* host, size_t bytes);

@@ -154,6 +154,14 @@ class PathTracer {
     check(fr_gaze_target(ctx(), g.data()), ctx_, "gaze_target");
     return g;
   }
+  float rebuild_bvh() {  // GPU LBVH over the current triangles (fr_rebuild_bvh), wall ms
+    float ms = 0.0f;
+    check(fr_rebuild_bvh(ctx(), &ms), ctx_, "rebuild_bvh");
+    return ms;
+  }
+  void set_positions(const float* xyz, size_t ntris) {  // moved vertices + GPU rebuild (fr_set_positions)
+    check(fr_set_positions(ctx(), xyz, ntris), ctx_, "set_positions");
+  }
   void set_gaze(float x, float y) {  // cursorPosCallback (FR/gui.cpp:48-66): window coordinates, y down
     check(fr_set_gaze(ctx(), x, y), ctx_, "set_gaze");
   }
