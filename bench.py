@@ -335,6 +335,9 @@ def main():
 
     # The timed region: K frames enqueued back to back. fr_frame pipelines them: frame N's
     # reconstruction (JFA/Sibson and pull-push/A-Trous streams) runs while frame N+1 traces.
+    # entry 3 (the roofline stage) is timed live inside the timed region: HIP events on the context
+    # stream around the stage and its megakernel, recorded by the library, no synchronisation added
+    tracer.kernel_timing(True)
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -344,6 +347,8 @@ def main():
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    live = tracer.kernel_times()
+    tracer.kernel_timing(False)
 
     st = tracer.stats()
     segs = st["segments"]
@@ -376,7 +381,15 @@ def main():
     # the dominant stage is entry 3 (shading_launch): k_shade_paths (path-trace megakernel) +
     # k_shade_resolve + k_carry_history; its algorithmic bytes are SURVEY §8(d)'s (56 + 4 rho) B/px.
     dominant = max(sb, key=lambda k: avg[k])
-    achieved = sb[dominant] / (avg[dominant] * 1e-3) / 1e9
+    launch_ms = avg[dominant]
+    kernel_ms = avg.get("shade_paths", 0.0)
+    timing_src = "HIP events on the context stream, serialised frames after the timed region"
+    if dominant == "shading" and live["frames"] > 0:
+        launch_ms = live["shading_ms"] / live["frames"]
+        kernel_ms = live["shade_paths_ms"] / live["frames"]
+        timing_src = (f"HIP events on the context stream around every entry-3 launch of the timed region "
+                      f"({live['frames']} pipelined frames)")
+    achieved = sb[dominant] / (launch_ms * 1e-3) / 1e9
     stage_kernels = {"shading": ["k_shade_paths", "k_shade_resolve", "k_carry_history"],
                      "geometry": ["k_gbuffer"], "sibson": ["k_sibson"]}
     image_stages = ["sampling", "optimize", "jfa", "sibson", "pullpush", "atrous"]
@@ -415,13 +428,15 @@ def main():
         "roofline": {"bound": "hbm", "kernel": f"{dominant} stage ({' + '.join(stage_kernels.get(dominant, []))})",
                      "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": None,
-                     "ms_per_launch": round(avg[dominant], 4),
+                     "ms_per_launch": round(launch_ms, 4),
                      "algorithmic_bytes_per_launch": int(sb[dominant]),
-                     "megakernel_ms": round(avg.get("shade_paths", 0.0), 4),
-                     "note": "achieved = SURVEY §8(d) algorithmic bytes of the stage / its HIP-event duration on the "
-                             "context stream (serialised frames after the timed region); the path-trace megakernel "
-                             "is latency/divergence bound (BVH pointer chasing), so Mrays/s is its figure of "
-                             "merit, image passes are HBM bound"},
+                     "megakernel_ms": round(kernel_ms, 4),
+                     "ms_per_launch_serialised": round(avg[dominant], 4),
+                     "megakernel_ms_serialised": round(avg.get("shade_paths", 0.0), 4),
+                     "timing": timing_src,
+                     "note": "achieved = SURVEY §8(d) algorithmic bytes of the stage / its average duration; the "
+                             "path-trace megakernel is latency/divergence bound (BVH pointer chasing), so Mrays/s "
+                             "is its figure of merit, image passes are HBM bound"},
         "roofline_image_passes": {"bound": "hbm", "achieved": round(img_bytes / (img_ms * 1e-3) / 1e9, 1),
                                   "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                   "frac": round(img_bytes / (img_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)},
@@ -430,7 +445,7 @@ def main():
     if traffic is not None:
         result["roofline"]["traffic"] = int(traffic)
         result["roofline"]["traffic_source"] = src
-        result["roofline"]["measured_hbm_GBs"] = round(traffic / (avg[dominant] * 1e-3) / 1e9, 1)
+        result["roofline"]["measured_hbm_GBs"] = round(traffic / (launch_ms * 1e-3) / 1e9, 1)
     # the GPU BVH builder on this scene (after every measurement: it replaces the BVH)
     builds = sorted(tracer.rebuild_bvh() for _ in range(3))
     result["bvh"] = {"builder": args.bvh, "gpu_rebuild_ms": round(builds[1], 3),

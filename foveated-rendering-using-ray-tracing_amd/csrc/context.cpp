@@ -117,6 +117,15 @@ struct fr_ctx {
   hipEvent_t ev[24] = {};  // 0-15 stage timing; 16 fork; 17 chain-2 join; 18, 19 reconstruction done per parity;
                            // 20-22 chain-1 timing
   bool time_kernels = false;  // fr_frame with timing: also time the path-trace kernel alone
+  // Live timing of entry 3 inside pipelined (untimed) frames: a ring of event quadruples recorded on
+  // the context stream around carry_history / k_shade_paths / resolve (fr_kernel_timing); a slot is
+  // harvested (its elapsed times summed) before it is reused and by fr_kernel_times.
+  static constexpr int KT_RING = 32;
+  hipEvent_t kt_ev[KT_RING][4] = {};
+  bool kt_on = false;
+  int kt_next = 0, kt_pending = 0;
+  uint32_t kt_frames = 0;
+  double kt_stage_ms = 0.0, kt_kernel_ms = 0.0;
   // scene export copies
   std::vector<const float*> tex_ptrs;
   std::vector<int32_t> tex_dims, mat_pairs;
@@ -244,6 +253,17 @@ bool invert_rowmajor(const float in[16], float out[16]) {  // Gauss-Jordan in f6
   for (int r = 0; r < 4; r++)
     for (int c = 0; c < 4; c++) out[r * 4 + c] = (float)a[r][c + 4];
   return true;
+}
+
+// Sums the elapsed times of ring slot i (its last event is synchronised first).
+void kt_harvest(fr_ctx* c, int i) {
+  hipEventSynchronize(c->kt_ev[i][3]);
+  float a = 0.0f, b = 0.0f;
+  hipEventElapsedTime(&a, c->kt_ev[i][0], c->kt_ev[i][3]);
+  hipEventElapsedTime(&b, c->kt_ev[i][1], c->kt_ev[i][2]);
+  c->kt_stage_ms += a;
+  c->kt_kernel_ms += b;
+  c->kt_frames++;
 }
 
 float elapsed(hipEvent_t a, hipEvent_t b) {
@@ -527,6 +547,8 @@ int fr_destroy(fr_ctx* c) {
   fr(c->mask); fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->jfa_a); fr(c->jfa_b);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
+  for (auto& q : c->kt_ev)
+    for (auto e : q) if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream3) hipStreamDestroy(c->stream3);
@@ -630,15 +652,27 @@ static int enqueue_shading(fr_ctx* c) {
     int rc = enqueue_optimize(c);
     if (rc) return rc;
   }
+  hipEvent_t* kt = nullptr;
+  if (c->kt_on) {
+    const int i = c->kt_next;
+    if (c->kt_pending == fr_ctx::KT_RING) { kt_harvest(c, i); c->kt_pending--; }
+    kt = c->kt_ev[i];
+    c->kt_next = (i + 1) % fr_ctx::KT_RING;
+    c->kt_pending++;
+    hipEventRecord(kt[0], c->stream);
+  }
   launch_carry_history(c->U, c->mask, c->img[P_WEIGHT], c->img[c->hist_cache], c->img[c->hist_cur],
                        c->img[P_shd(c)], c->stream);
   const uint32_t N = (uint32_t)((size_t)c->W * c->H);
   if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
+  if (kt) hipEventRecord(kt[1], c->stream);
   launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache],
                      c->shade_ctr, c->samples, c->stats, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
+  if (kt) hipEventRecord(kt[2], c->stream);
   launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache], c->samples,
                        c->img[c->hist_cur], c->img[P_shd(c)], c->stream);
+  if (kt) hipEventRecord(kt[3], c->stream);
   int rc = check_launch(c);
   // swapBuffer("history_cache", "history_buffer"); swapBuffer("depth_cache", "depth_buffer") (:226-227)
   std::swap(c->hist_cur, c->hist_cache);
@@ -1075,6 +1109,28 @@ int fr_get_stats(fr_ctx* c, fr_stats* s) {
   s->reflection = d.reflection; s->truncated = d.truncated; s->overflow = d.bvh_overflow;
   for (int i = 0; i < 6; i++) s->diag[i] = d.pad[i];
   s->segments = d.gbuffer_primary + d.primary + d.shadow + d.diffuse_bounce + d.mirror + d.refraction + d.reflection;
+  return FR_OK;
+}
+
+int fr_kernel_timing(fr_ctx* c, int enable) {
+  if (!c) return FR_E_INVALID;
+  if (enable && !c->kt_ev[0][0])
+    for (auto& q : c->kt_ev)
+      for (auto& e : q) HIP_TRY(c, hipEventCreate(&e));
+  c->kt_on = enable != 0;
+  c->kt_next = c->kt_pending = 0;
+  c->kt_frames = 0;
+  c->kt_stage_ms = c->kt_kernel_ms = 0.0;
+  return FR_OK;
+}
+
+int fr_kernel_times(fr_ctx* c, fr_stage_times* out) {
+  if (!c || !out) return FR_E_INVALID;
+  for (; c->kt_pending > 0; c->kt_pending--)
+    kt_harvest(c, (c->kt_next - c->kt_pending + fr_ctx::KT_RING) % fr_ctx::KT_RING);
+  out->frames = c->kt_frames;
+  out->shading_ms = c->kt_stage_ms;
+  out->shade_paths_ms = c->kt_kernel_ms;
   return FR_OK;
 }
 

@@ -83,6 +83,10 @@ class fr_frame_timing(C.Structure):
                [("ray_count", C.c_uint32), ("shade_paths_ms", C.c_float)]
 
 
+class fr_stage_times(C.Structure):
+    _fields_ = [("frames", C.c_uint32), ("shading_ms", C.c_double), ("shade_paths_ms", C.c_double)]
+
+
 class fr_scene_arrays(C.Structure):
     _fields_ = [("num_tris", C.c_int), ("pos", C.POINTER(C.c_float)), ("nrm", C.POINTER(C.c_float)),
                 ("uv", C.POINTER(C.c_float)), ("flags", C.POINTER(C.c_int32)), ("num_materials", C.c_int),
@@ -138,6 +142,8 @@ _SIGS = {
     "fr_set_positions": [C.c_void_p, C.POINTER(C.c_float), C.c_size_t],
     "fr_get_stats": [C.c_void_p, C.POINTER(fr_stats)],
     "fr_reset_stats": [C.c_void_p],
+    "fr_kernel_timing": [C.c_void_p, C.c_int],
+    "fr_kernel_times": [C.c_void_p, C.POINTER(fr_stage_times)],
     "fr_scene_export": [C.c_void_p, C.POINTER(fr_scene_arrays)],
     "fr_scene_create": [C.POINTER(fr_config), C.POINTER(C.c_void_p)],
     "fr_scene_get_arrays": [C.c_void_p, C.POINTER(fr_scene_arrays)],
@@ -414,6 +420,16 @@ class PathTracer:
 
     def reset_stats(self):
         self._check(_lib.fr_reset_stats(self._ctx))
+
+    def kernel_timing(self, enable: bool):
+        """Starts (or stops) the live HIP-event timing of entry 3 inside pipelined frames."""
+        self._check(_lib.fr_kernel_timing(self._ctx, 1 if enable else 0))
+
+    def kernel_times(self) -> dict:
+        """{frames, shading_ms, shade_paths_ms}: stages timed since kernel_timing(True), summed ms."""
+        t = fr_stage_times()
+        self._check(_lib.fr_kernel_times(self._ctx, C.byref(t)))
+        return {"frames": t.frames, "shading_ms": t.shading_ms, "shade_paths_ms": t.shade_paths_ms}
 
     def _frame(self, fn, timing):
         t = fr_frame_timing() if timing else None

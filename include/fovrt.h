@@ -247,6 +247,19 @@ int fr_copy_buffer(fr_ctx* ctx, int id, void* device_dst, size_t bytes);  /* dev
 int fr_get_stats(fr_ctx* ctx, fr_stats* stats);
 int fr_reset_stats(fr_ctx* ctx);
 
+/* Live timing of entry 3 inside pipelined frames (no synchronisation added): after
+ * fr_kernel_timing(ctx, 1) every shading stage records HIP events on the context stream around
+ * itself and around the path-trace megakernel; fr_kernel_times returns the number of stages timed
+ * since and their summed milliseconds (what rocprofv3 --kernel-trace reports for k_shade_paths).
+ * fr_kernel_timing(ctx, 0) stops and clears. */
+typedef struct fr_stage_times {
+  uint32_t frames;
+  double shading_ms;      /* carry_history + k_shade_paths + k_shade_resolve, summed */
+  double shade_paths_ms;  /* k_shade_paths alone, summed */
+} fr_stage_times;
+int fr_kernel_timing(fr_ctx* ctx, int enable);
+int fr_kernel_times(fr_ctx* ctx, fr_stage_times* out);
+
 /* Scene inspection (host copies owned by the context; valid until fr_destroy). */
 typedef struct fr_scene_arrays {
   int num_tris;
