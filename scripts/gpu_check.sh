@@ -1,0 +1,8 @@
+#!/bin/bash
+# GPU parity suite + one bench line: scripts/gpu_check.sh [pytest -k expr]
+set -o pipefail
+mkdir -p gpurun_out
+K=${1:-}
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${K:+-k "$K"} > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/ab_default.log 2>&1 || exit 2
