@@ -9,4 +9,4 @@ timeout -k 10 200 python3 "$ROOT/scripts/stage_probe.py" 10 > "$OUT/probe.txt" 2
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
-  python3 "$ROOT/scripts/stage_probe.py" 5 > "$OUT/probe_prof.txt" 2>&1
+  python3 "$ROOT/scripts/stage_probe.py" 30 > "$OUT/probe_prof.txt" 2>&1
