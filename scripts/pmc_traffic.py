@@ -62,6 +62,23 @@ def main():
             bench = json.loads(f.read().strip().splitlines()[-1])
     except (OSError, ValueError, IndexError):
         pass
+    # the roofline stage's kernels over the timed region only: bench.py runs `warmup` pipelined frames,
+    # `steps` timed pipelined frames, then serialised stage frames; one k_shade_paths per frame
+    timed = {}
+    try:
+        trace = find(os.path.join(out_dir, "trace"), "*kernel_trace.csv")
+        steps, warmup = bench.get("steps", 20), bench.get("warmup", 5)
+        per = {}
+        with open(trace) as f:
+            for row in csv.DictReader(f):
+                per.setdefault(short(row["Kernel_Name"]), []).append(
+                    (int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+        for k in ("k_shade_paths", "k_shade_resolve", "k_carry_history"):
+            d = [ns for _, ns in sorted(per.get(k, []))][warmup:warmup + steps]
+            if d:
+                timed[k] = {"dispatches": len(d), "avg_ns": sum(d) / len(d)}
+    except SystemExit:
+        pass
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
         fr_kib, n = fetch.get(k, (0.0, 0))
@@ -77,7 +94,10 @@ def main():
     doc = {"tag": tag, "bench_args": bench_args, "config": bench.get("config"),
            "correction": "hbm_read_bytes = 2 x FETCH_SIZE (gfx950 half-count of wide streaming reads); "
                          "hbm_write_bytes = WRITE_SIZE; both per dispatch, averaged over the profiled dispatches",
-           "kernels": kernels}
+           "kernels": kernels,
+           "timed_region": timed,
+           "timed_region_note": "kernel-trace durations of the roofline stage's kernels over the bench's timed "
+                                "(pipelined) frames only; bench.py's live HIP-event average covers the same frames"}
     with open(os.path.join(root, "profiles", f"{tag}_pmc_traffic.json"), "w") as f:
         json.dump(doc, f, indent=1)
     for k, e in sorted(kernels.items(), key=lambda kv: -kv[1].get("avg_ns", 0)):

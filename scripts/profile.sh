@@ -1,6 +1,7 @@
 #!/bin/bash
 # Per-round profile of the bench workload on the GPU box (run through gpurun):
-#   1. rocprofv3 --kernel-trace --stats      -> per-kernel average durations
+#   1. rocprofv3 --kernel-trace --stats      -> per-kernel average durations (the default bench command;
+#                                               the CPU baseline launches no kernel and is skipped)
 #   2. rocprofv3 --pmc FETCH_SIZE            -> HBM read bytes per dispatch   (own pass)
 #   3. rocprofv3 --pmc WRITE_SIZE            -> HBM write bytes per dispatch  (own pass)
 #   4. scripts/pmc_traffic.py                -> profiles/<tag>_pmc_traffic.json (read by bench.py)
@@ -14,7 +15,7 @@ mkdir -p "$OUT" "$ROOT/profiles"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 420 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
-  python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline "$@" > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
+  python3 "$ROOT/bench.py" --no-cpu-baseline "$@" > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE -f csv -d "$OUT/fetch" -o run -- \
   python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline "$@" > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
 timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE -f csv -d "$OUT/write" -o run -- \
