@@ -1112,6 +1112,9 @@ int fr_get_stats(fr_ctx* c, fr_stats* s) {
   return FR_OK;
 }
 
+// Test hook (not part of include/fovrt.h): the host build of the bound JFA and Sibson use.
+float fr__sqrt_le_bound(float s) { return sqrt_le_bound(s); }
+
 int fr_kernel_timing(fr_ctx* c, int enable) {
   if (!c) return FR_E_INVALID;
   if (enable && !c->kt_ev[0][0])

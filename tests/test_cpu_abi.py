@@ -250,3 +250,21 @@ def test_obj_meshes_replace_the_stand_ins(fovrt_mod, tmp_path):
     with pytest.raises(fovrt_mod.FovrtError):
         fovrt_mod.Scene(fovrt_mod.Config(scene=fovrt_mod.SCENE_BOX, texture_mode=1, mesh_mode=2,
                                          asset_dir=str(bad))).arrays()
+
+
+def test_sqrt_le_bound_is_the_largest_float_whose_sqrt_is_at_most_s(fovrt_mod):
+    """The closed-form bound (fr_math.h) JFA and Sibson compare squared distances against: the host
+    build of the same source, checked against correctly rounded float32 sqrt on random and edge values."""
+    lib = fovrt_mod.load_library()
+    fn = lib.fr__sqrt_le_bound
+    fn.argtypes, fn.restype = [C.c_float], C.c_float
+    rng = np.random.default_rng(20180920)
+    xs = np.concatenate([rng.random(20000, dtype=np.float32) * np.float32(4.0),
+                         rng.random(20000, dtype=np.float32) * np.float32(1e-6),
+                         (rng.integers(0, 4096, 20000) / np.float32(3840.0)).astype(np.float32) ** 2,
+                         np.array([0.0, 1e-30, 1.0, 2.0, 0.25, 3.999999], np.float32)])
+    s = np.sqrt(xs).astype(np.float32)  # float32 sqrt: correctly rounded
+    b = np.array([fn(float(v)) for v in s], np.float32)
+    assert (np.sqrt(b) <= s).all()
+    nxt = np.nextafter(b, np.float32(np.inf))
+    assert (np.sqrt(nxt) > s).all()
