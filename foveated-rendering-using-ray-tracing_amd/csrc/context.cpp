@@ -416,9 +416,17 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   c->W = cfg.width; c->H = cfg.height;
   auto bail = [&](int code) { g_create_error = c->err; fr_destroy(c); return code; };
   if (hipSetDevice(cfg.device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(FR_E_HIP); }
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
+  // The trace half (context stream) is the frame's critical path; the reconstruction streams have a
+  // frame of slack (FOVRT_STREAM_PRIORITY=0: all streams at the default priority).
+  int prio_lo = 0, prio_hi = 0;
+  static const bool use_prio = [] {
+    const char* v = getenv("FOVRT_STREAM_PRIORITY");
+    return !v || atoi(v) != 0;
+  }();
+  if (use_prio) hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess) {
     c->err = "stream create failed";
     return bail(FR_E_HIP);
   }
