@@ -23,7 +23,7 @@ void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f
 void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
                         const f4*, uint32_t*, f4*, DevStats*, hipStream_t);
 void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
-                          const f4*, f4*, f4*, hipStream_t);
+                          const f4*, f4*, f4*, uint32_t*, hipStream_t);
 size_t shade_counter_words();
 void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
 void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
@@ -679,7 +679,7 @@ static int enqueue_shading(fr_ctx* c) {
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   if (kt) hipEventRecord(kt[2], c->stream);
   launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache], c->samples,
-                       c->img[c->hist_cur], c->img[P_shd(c)], c->stream);
+                       c->img[c->hist_cur], c->img[P_shd(c)], c->shade_ctr, c->stream);
   if (kt) hipEventRecord(kt[3], c->stream);
   int rc = check_launch(c);
   // swapBuffer("history_cache", "history_buffer"); swapBuffer("depth_cache", "depth_buffer") (:226-227)
