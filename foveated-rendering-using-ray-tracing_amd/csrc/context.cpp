@@ -70,6 +70,7 @@ struct fr_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // reconstruction chain 2: pull-push -> A-Trous
   hipStream_t stream3 = nullptr;  // reconstruction chain 1: JFA -> Sibson
+  hipStream_t stream4 = nullptr;  // entry 3's carry of the inactive pixels, beside the megakernel
   // Frame pipelining: frame N's reconstruction (stream3 + stream2) runs while frame N+1 traces on
   // `stream`. The buffers the reconstruction reads (POSITION, NORMAL, SHADING) alternate by frame
   // parity `par`; the trace half of a frame waits for the reconstruction that last read its parity.
@@ -426,7 +427,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (use_prio) hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_lo) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) != hipSuccess) {
     c->err = "stream create failed";
     return bail(FR_E_HIP);
   }
@@ -547,6 +549,7 @@ int fr_destroy(fr_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->stream2) hipStreamSynchronize(c->stream2);
   if (c->stream3) hipStreamSynchronize(c->stream3);
+  if (c->stream4) hipStreamSynchronize(c->stream4);
   auto fr = [](void* p) { if (p) hipFree(p); };
   fr(c->d_nodes); fr(c->d_tri); fr(c->d_prim); fr(c->d_shade); fr(c->d_pos);
   for (auto p : c->d_tex) fr(p);
@@ -560,6 +563,7 @@ int fr_destroy(fr_ctx* c) {
   if (c->stream) hipStreamDestroy(c->stream);
   if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream3) hipStreamDestroy(c->stream3);
+  if (c->stream4) hipStreamDestroy(c->stream4);
   delete c;
   return FR_OK;
 }
@@ -669,8 +673,13 @@ static int enqueue_shading(fr_ctx* c) {
     c->kt_pending++;
     hipEventRecord(kt[0], c->stream);
   }
+  // The inactive pixels' history carry (HBM-bound) touches no buffer k_shade_paths reads or writes:
+  // it runs on stream4 beside the latency-bound megakernel and joins before the resolve.
+  hipEventRecord(c->ev[11], c->stream);
+  hipStreamWaitEvent(c->stream4, c->ev[11], 0);
   launch_carry_history(c->U, c->mask, c->img[P_WEIGHT], c->img[c->hist_cache], c->img[c->hist_cur],
-                       c->img[P_shd(c)], c->stream);
+                       c->img[P_shd(c)], c->stream4);
+  hipEventRecord(c->ev[12], c->stream4);
   const uint32_t N = (uint32_t)((size_t)c->W * c->H);
   if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
   if (kt) hipEventRecord(kt[1], c->stream);
@@ -678,6 +687,7 @@ static int enqueue_shading(fr_ctx* c) {
                      c->shade_ctr, c->samples, c->stats, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   if (kt) hipEventRecord(kt[2], c->stream);
+  hipStreamWaitEvent(c->stream, c->ev[12], 0);
   launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache], c->samples,
                        c->img[c->hist_cur], c->img[P_shd(c)], c->shade_ctr, c->stream);
   if (kt) hipEventRecord(kt[3], c->stream);
