@@ -21,7 +21,9 @@
 namespace fr {
 void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
 void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
-                        const f4*, uint32_t*, f4*, DevStats*, hipStream_t);
+                        const f4*, uint32_t*, f4*, DevStats*, f4*, uint32_t*, hipStream_t);
+void launch_sample_setup(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*, f4*,
+                         uint32_t*, hipStream_t);
 void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
                           const f4*, f4*, f4*, uint32_t*, hipStream_t);
 size_t shade_counter_words();
@@ -106,6 +108,8 @@ struct fr_ctx {
   uint32_t* active = nullptr;
   uint32_t* shade_ctr = nullptr;  // sharded chunk counters of the shading work queue
   f4* samples = nullptr;          // one radiance value per (active pixel, camera sample)
+  f4* aux = nullptr;              // per active pixel: NDC position, r1, r2 (k_sample_setup)
+  uint32_t* aux_seed = nullptr;   // per active pixel: the seed after the two draws
   u2 *jfa_a = nullptr, *jfa_b = nullptr;  // JFA state ping-pong (seed coord texel + alpha flags)
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
   int pp_S = 0;
@@ -509,7 +513,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       dalloc(&c->active, N) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
       dalloc(&c->pull, atlas) != hipSuccess || dalloc(&c->push, atlas) != hipSuccess ||
       dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess ||
-      dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, N * cfg.spp) != hipSuccess) {
+      dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, N * cfg.spp) != hipSuccess ||
+      dalloc(&c->aux, N) != hipSuccess || dalloc(&c->aux_seed, N) != hipSuccess) {
     c->err = "device allocation (work buffers) failed";
     return bail(FR_E_NOMEM);
   }
@@ -555,7 +560,7 @@ int fr_destroy(fr_ctx* c) {
   for (auto p : c->d_tex) fr(p);
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
-  fr(c->mask); fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->jfa_a); fr(c->jfa_b);
+  fr(c->mask); fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->aux); fr(c->aux_seed); fr(c->jfa_a); fr(c->jfa_b);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   for (auto& q : c->kt_ev)
@@ -681,10 +686,12 @@ static int enqueue_shading(fr_ctx* c) {
                        c->img[P_shd(c)], c->stream4);
   hipEventRecord(c->ev[12], c->stream4);
   const uint32_t N = (uint32_t)((size_t)c->W * c->H);
+  launch_sample_setup(c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache], c->aux, c->aux_seed,
+                      c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
   if (kt) hipEventRecord(kt[1], c->stream);
   launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache],
-                     c->shade_ctr, c->samples, c->stats, c->stream);
+                     c->shade_ctr, c->samples, c->stats, c->aux, c->aux_seed, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   if (kt) hipEventRecord(kt[2], c->stream);
   hipStreamWaitEvent(c->stream, c->ev[12], 0);
