@@ -179,6 +179,9 @@ class PathTracer {
     return v;
   }
   fr_stats stats() { fr_stats s{}; check(fr_get_stats(ctx(), &s), ctx_, "stats"); return s; }
+  // live per-launch HIP-event timing of the shading stage (off by default)
+  void kernel_timing(bool on) { check(fr_kernel_timing(ctx(), on ? 1 : 0), ctx_, "kernel_timing"); }
+  fr_stage_times kernel_times() { fr_stage_times t{}; check(fr_kernel_times(ctx(), &t), ctx_, "kernel_times"); return t; }
   fr_ctx* ctx() const {
     if (!ctx_) throw Error(FR_E_STATE, "PathTracer used before initialize()");
     return ctx_;

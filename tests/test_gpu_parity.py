@@ -230,6 +230,23 @@ def test_frame_driver_equals_stage_calls(fovrt_mod, timing):
         assert equal_nan(a.read(tid), b.read(tid)), tid
 
 
+def test_kernel_timing_counts_frames_and_leaves_results_unchanged(fovrt_mod):
+    """fr_kernel_timing: live HIP events around entry 3 of pipelined frames (what bench.py reports)."""
+    W, H, K = 128, 128, 40  # more frames than the 32-slot event ring: slots are harvested on reuse
+    a = make_tracer(fovrt_mod, W, H, scene=1, mask=1, spp=4, dmd=3)
+    b = make_tracer(fovrt_mod, W, H, scene=1, mask=1, spp=4, dmd=3)
+    a.kernel_timing(True)
+    for _ in range(K):
+        a.frame(timing=False)
+        b.frame(timing=False)
+    kt = a.kernel_times()
+    a.kernel_timing(False)
+    assert kt["frames"] == K
+    assert kt["shading_ms"] >= kt["shade_paths_ms"] > 0
+    for tid in (TN.SHADING, TN.SIBSON, TN.ATROUS, TN.HISTORY_CACHE):
+        assert equal_nan(a.read(tid), b.read(tid)), tid
+
+
 def test_full_size_frame_properties(fovrt_mod):
     """BASELINE configs[2] at its full size (bunny, 3840x2160, 4 spp, GI 3, 10% log-polar mask):
     size-independent invariants of every stage."""
