@@ -124,6 +124,29 @@ def test_shading_within_tolerance(fovrt_mod, oracle, scene, spp, dmd, mask_mode)
     assert st["overflow"] == 0 and st["primary"] > 0
 
 
+@pytest.mark.parametrize("refr", [0, 1, 3])
+def test_shading_refraction_depth_cap(fovrt_mod, oracle, refr):
+    """Glass bunny with the refraction recursion cut short (fr_config.refraction_max_depth): the
+    truncation path and refraction nodes that keep one child or none, against the oracle at the same cap."""
+    W, H, spp = 64, 48, 4
+    t = make_tracer(fovrt_mod, W, H, scene=1, mask=3, spp=spp, dmd=3, refr=refr)
+    uni = fovrt_mod.Camera.preset(1, W, H).uniforms(W, H)
+    t.set_camera_uniforms(uni)
+    osc = oracle.OracleScene(t.scene_arrays(), refraction_max_depth=refr, diffuse_max_depth=3)
+    frame = t.m_accumFrame
+    t.geometry_launch(); t.sampling_launch(); t.optimize_launch()
+    mask, weight, hist_in = t.read(TN.MASK), t.read(TN.WEIGHT), t.read(TN.HISTORY_CACHE)
+    t.shading_launch()
+    got = t.read(TN.SHADING)
+    ref = oracle.shading(osc, uni, W, H, frame, spp, mask, weight, hist_in)
+    rm = rmse_per_channel(got, ref["shading"])
+    assert (rm <= 1e-3).all(), (rm, mismatch_report(got, ref["shading"]))
+    st = t.stats()
+    assert st["truncated"] > 0 and st["overflow"] == 0
+    if refr == 0:
+        assert st["refraction"] == 0 and st["reflection"] == 0
+
+
 # ---------------------------------------------------------------------------------------------
 # JumpFlooding / Sibson / PullPush — bit-exact; A-Trous — tolerance
 # ---------------------------------------------------------------------------------------------
