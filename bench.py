@@ -110,6 +110,17 @@ def reduce_over_ranks(dist, device, elapsed, segs):
     return float(t.item()), float(s.item())
 
 
+def view_segments(st, G, vrank):
+    """Ray segments a rank contributes to `value`, and its redundant ones. A tile-sharded view (G > 1)
+    traces its full G-buffer on every one of its G ranks (the saliency stencils and the root's A-Trous
+    read all of it): those W*H primaries count once per view, on the view's first rank; the other
+    ranks' copies are reported apart as redundant work, never as throughput."""
+    segs = int(st["segments"])
+    if G > 1 and vrank != 0:
+        return segs - int(st["gbuffer_primary"]), int(st["gbuffer_primary"])
+    return segs, 0
+
+
 def view_layout(rank, world, views):
     """Ranks -> views: `views` views of world / views ranks each; the ranks of a view tile-shard it
     and composite on the view's first rank. Returns (view, rank in view, ranks per view)."""
@@ -351,11 +362,12 @@ def main():
     tracer.kernel_timing(False)
 
     st = tracer.stats()
-    segs = st["segments"]
+    segs, redundant = view_segments(st, G, vrank)
     dev = None
     if dist is not None:
         dev = torch.device("cuda", device) if has_gpu and dist.get_backend() == "nccl" else torch.device("cpu")
     elapsed, total_segs = reduce_over_ranks(dist, dev, elapsed, segs)
+    _, total_redundant = reduce_over_ranks(dist, dev, 0.0, redundant)
 
     # Per-stage HIP-event breakdown of the same frames, serialised (each frame synchronised, so the
     # stage times do not overlap the next frame): the stage table and the roofline kernel time.
@@ -422,6 +434,8 @@ def main():
         "frames_per_s_total": round(views * K / elapsed, 2),
         "rays": {k: st[k] for k in ("gbuffer_primary", "primary", "shadow", "diffuse_bounce", "mirror",
                                     "refraction", "reflection", "truncated", "overflow")},
+        "rays_note": "rank 0's counters over the timed frames",
+        "gbuffer_redundant_segments": int(total_redundant),
         "stages": stage_table,
         "stages_note": f"HIP events, {n_timed} serialised frames; the timed region pipelines frame N's reconstruction "
                        "with frame N+1's trace half, so ms_per_step < the sum of the stages",

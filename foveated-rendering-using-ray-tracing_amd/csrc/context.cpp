@@ -380,20 +380,33 @@ static int gpu_rebuild(fr_ctx* c) {
     c->err = "GPU BVH needs a traversal stack deeper than FR_BVH_STACK";
     return FR_E_UNSUPPORTED;
   }
-  if (c->d_nodes) hipFree(c->d_nodes);
-  if (c->d_tri) hipFree(c->d_tri);
-  if (c->d_prim) hipFree(c->d_prim);
-  c->d_nodes = nodes; c->d_tri = tri; c->d_prim = prim;
-  c->dsc.nodes = nodes; c->dsc.tri_geo = tri; c->dsc.tri_prim = prim;
-  Bvh& b = c->bvh;
+  // host mirror first: the context switches to the new tree only when every step succeeded
+  Bvh b;
   b.nodes.resize(nn); b.tri_geo.resize(nt); b.tri_prim.resize(nt);
   b.root_count = 0; b.max_stack = max_stack; b.max_depth = 0;
   if (hipMemcpy(b.nodes.data(), nodes, (size_t)nn * sizeof(BvhNode), hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(b.tri_geo.data(), tri, (size_t)nt * sizeof(TriGeo), hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(b.tri_prim.data(), prim, (size_t)nt * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) {
+    hipFree(nodes); hipFree(tri); hipFree(prim);
     c->err = "GPU BVH: readback failed";
     return FR_E_HIP;
   }
+  if (c->d_nodes) hipFree(c->d_nodes);
+  if (c->d_tri) hipFree(c->d_tri);
+  if (c->d_prim) hipFree(c->d_prim);
+  c->d_nodes = nodes; c->d_tri = tri; c->d_prim = prim;
+  c->dsc.nodes = nodes; c->dsc.tri_geo = tri; c->dsc.tri_prim = prim;
+  // tree depth (fr_scene_info.bvh_depth) of the four-wide tree: the inner entries have count 0
+  std::vector<std::pair<int, int>> todo{{0, 0}};
+  while (!todo.empty()) {
+    const auto [ni, depth] = todo.back();
+    todo.pop_back();
+    b.max_depth = std::max(b.max_depth, depth);
+    for (int k = 0; k < 4; k++)
+      if (b.nodes[ni].count[k] == 0 && b.nodes[ni].child[k] > ni && b.nodes[ni].child[k] < nn)
+        todo.push_back({b.nodes[ni].child[k], depth + 1});
+  }
+  c->bvh = std::move(b);
   return FR_OK;
 }
 
@@ -580,6 +593,7 @@ int fr_set_camera(fr_ctx* c, const fr_camera* cam) {
   memcpy(U.prev_vp.m, cam->prev_vp, sizeof(U.prev_vp.m));
   U.eye = mk3(cam->eye[0], cam->eye[1], cam->eye[2]);
   U.prev_eye = mk3(cam->prev_eye[0], cam->prev_eye[1], cam->prev_eye[2]);
+  if (!std::isfinite(cam->gaze[0]) || !std::isfinite(cam->gaze[1])) return fail(c, FR_E_INVALID, "fr_set_camera: gaze not finite");
   U.gaze = mk2(cam->gaze[0], cam->gaze[1]);
   return FR_OK;
 }
@@ -831,7 +845,9 @@ int fr_composite_views(fr_ctx* c, const void* views, int nviews, void* out, size
 int fr_set_gaze(fr_ctx* c, float x, float y) {
   // cursorPosCallback (FR/gui.cpp:48-66) sets g_gaze in window coordinates (y down); the kernels
   // use (g_gaze.x, H - g_gaze.y) (FR/PathTracer.cpp:796-797)
-  if (!c) return FR_E_INVALID;
+  if (!c || !std::isfinite(x) || !std::isfinite(y)) return FR_E_INVALID;
+  // off-window cursors are kept as given (the log-polar mask and the gaze distance are defined for
+  // any gaze); the two texel reads at the gaze clamp to the screen (k_sampling, fr_gaze_target)
   c->U.gaze = mk2(x, (float)c->H - y);
   return FR_OK;
 }
@@ -980,8 +996,8 @@ int fr_gaze_target(fr_ctx* c, float xyz[3]) {
   // gaze_target[0] = position_buffer[make_uint2(gaze)] (samplingStep.cu:184)
   if (!c || !xyz) return FR_E_INVALID;
   join_recon(c);
-  uint32_t gx = f2u_sat(c->U.gaze.x), gy = f2u_sat(c->U.gaze.y);
-  if (gx >= (uint32_t)c->W || gy >= (uint32_t)c->H) return fail(c, FR_E_STATE, "gaze outside the screen");
+  // same texel as the sampling kernel's focal-depth read: saturating conversion, clamped to the screen
+  const uint32_t gx = std::min(f2u_sat(c->U.gaze.x), (uint32_t)c->W - 1), gy = std::min(f2u_sat(c->U.gaze.y), (uint32_t)c->H - 1);
   f4 v;
   HIP_TRY(c, hipMemcpyAsync(&v, c->img[P_pos(c)] + (size_t)gy * c->W + gx, sizeof(f4), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1047,12 +1063,32 @@ static_assert(sizeof(f3) == 3 * sizeof(float), "f3 must be three packed floats")
 int fr_set_positions(fr_ctx* c, const float* xyz, size_t ntris) {
   if (!c || !xyz) return FR_E_INVALID;
   if (ntris != (size_t)c->scene.num_tris()) return fail(c, FR_E_INVALID, "fr_set_positions: triangle count differs");
+  for (size_t i = 0; i < ntris * 9; i++)
+    if (!std::isfinite(xyz[i])) return fail(c, FR_E_INVALID, "fr_set_positions: position not finite");
   join_recon(c);
   hipSetDevice(c->cfg.device);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  memcpy(c->scene.pos.data(), xyz, ntris * 9 * sizeof(float));
-  HIP_TRY(c, hipMemcpy(c->d_pos, xyz, ntris * 9 * sizeof(float), hipMemcpyHostToDevice));
-  return gpu_rebuild(c);
+  // the BVH is built from the device copy; the context commits the new positions (host mirror,
+  // bounding box) only once the rebuild succeeded, and puts the old device copy back otherwise
+  const size_t bytes = ntris * 9 * sizeof(float);
+  HIP_TRY(c, hipMemcpy(c->d_pos, xyz, bytes, hipMemcpyHostToDevice));
+  if (const int rc = gpu_rebuild(c)) {
+    const std::string why = c->err;
+    if (hipMemcpy(c->d_pos, c->scene.pos.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(c, FR_E_HIP, "fr_set_positions: rebuild failed (" + why + ") and the old positions could not be restored");
+    return fail(c, rc, "fr_set_positions: rebuild failed, scene unchanged: " + why);
+  }
+  memcpy(c->scene.pos.data(), xyz, bytes);
+  // bbox_min / bbox_max (the depth-saliency theta of k_sampling) follow the geometry, as the
+  // reference's scene AABB does at load time (FR/PathTracer.cpp:601-602,663)
+  f3 lo = mk3(INFINITY), hi = mk3(-INFINITY);
+  for (const f3& v : c->scene.pos) {
+    lo = mk3(fminf(lo.x, v.x), fminf(lo.y, v.y), fminf(lo.z, v.z));
+    hi = mk3(fmaxf(hi.x, v.x), fmaxf(hi.y, v.y), fmaxf(hi.z, v.z));
+  }
+  c->scene.bbox_min = c->dsc.bbox_min = lo;
+  c->scene.bbox_max = c->dsc.bbox_max = hi;
+  return FR_OK;
 }
 
 #ifdef FR_STAMPS

@@ -95,3 +95,16 @@ def test_view_layout():
     assert bench.view_layout(3, 4, 1) == (0, 3, 4)   # one view tiled over 4 ranks
     with pytest.raises(SystemExit):
         bench.view_layout(0, 6, 4)
+
+
+def test_view_segments_count_the_gbuffer_once_per_view():
+    """Tile sharding: every rank of a view traces the full G-buffer; value counts it once (vrank 0)."""
+    import bench
+    st = {"segments": 1000, "gbuffer_primary": 600}
+    assert bench.view_segments(st, 1, 0) == (1000, 0)     # one view per rank: everything counts
+    assert bench.view_segments(st, 4, 0) == (1000, 0)     # the view's first rank keeps its G-buffer
+    assert bench.view_segments(st, 4, 3) == (400, 600)    # the others' copies are redundant work
+    W, H, G = 64, 32, 4                                   # summed over a view: W*H primaries once
+    ranks = [{"segments": W * H + 10 * r, "gbuffer_primary": W * H} for r in range(G)]
+    total = sum(bench.view_segments(s, G, r)[0] for r, s in enumerate(ranks))
+    assert total == W * H + sum(10 * r for r in range(G))

@@ -162,3 +162,35 @@ def test_sqrt_free_disc_test_is_exact():
         for r2 in probe:
             r2 = np.float32(r2)
             assert (np.sqrt(r2) > d) == (r2 > b), (d, r2, b)
+
+
+# ---------------------------------------------------------------------------------------------
+# Pull-push and A-Trous: the oracle against independent numpy restatements written from the
+# reference's GLSL (tests/helpers.py), so the GPU's bit-exact pull-push and its A-Trous tolerance
+# rest on two restatements of the shaders, not on the oracle alone (parity is still unpinned
+# against the reference itself: it cannot run here and ships no outputs).
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("W,H", [(16, 16), (32, 32), (24, 20), (1, 1), (64, 40)])
+def test_pullpush_oracle_equals_numpy_restatement(oracle, W, H):
+    from helpers import PullPushNp
+    rng = np.random.default_rng(W * 7 + H)
+    ref, mine = oracle.PullPushState(W, H), PullPushNp(W, H)
+    for k, p in enumerate((0.1, 0.02, 0.4, 0.0, 1.0)):  # atlases carry state across frames
+        img = sparse_image(W, H, (rng.random((H, W)) < p).astype(np.uint8), seed=k)
+        a, b = ref.render(img), mine.render(img)
+        assert equal_nan(a, b), (k, np.argwhere(~np.isclose(a, b, rtol=0, atol=0, equal_nan=True))[:4])
+        assert equal_nan(ref.push, mine.push) and equal_nan(ref.pull, mine.pull)
+
+
+@pytest.mark.parametrize("W,H,count", [(32, 24, 1), (40, 33, 2), (17, 9, 3)])
+def test_atrous_oracle_matches_numpy_restatement(oracle, W, H, count):
+    from helpers import atrous_np
+    rng = np.random.default_rng(W + H + count)
+    pos = rng.normal(size=(H, W, 4)).astype(np.float32) * np.float32(0.3)
+    pos[..., 3] = 1.0
+    nrm = rng.random((H, W, 4), dtype=np.float32)
+    nrm[..., 3] = (rng.random((H, W)) < 0.5).astype(np.float32)
+    col = rng.random((H, W, 4), dtype=np.float32)
+    got = oracle.atrous(count, pos, nrm, col)
+    ref = atrous_np(count, pos, nrm, col)
+    assert np.abs(got - ref).max() <= 2e-6, np.abs(got - ref).max()

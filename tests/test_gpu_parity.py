@@ -9,8 +9,8 @@ never leaks into the next stage's comparison.
 import numpy as np
 import pytest
 
-from helpers import (GOLDEN, TEXTURE_MODE, ASSET_DIR, equal_nan, logpolar_mask_np, rmse_per_channel,
-                     sparse_image)
+from helpers import (GOLDEN, TEXTURE_MODE, ASSET_DIR, PullPushNp, atrous_np, equal_nan, logpolar_mask_np,
+                     rmse_per_channel, sparse_image)
 
 pytestmark = pytest.mark.gpu
 
@@ -42,9 +42,8 @@ def mismatch_report(a, b):
 # ---------------------------------------------------------------------------------------------
 # entry 0 — G-buffer (bit-exact)
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("scene", [0, 1, 2])
-def test_gbuffer_bit_exact(fovrt_mod, oracle, scene):
-    W, H = 96, 64
+@pytest.mark.parametrize("scene,W,H", [(0, 96, 64), (1, 96, 64), (2, 96, 64), (1, 100, 70)])
+def test_gbuffer_bit_exact(fovrt_mod, oracle, scene, W, H):
     t = make_tracer(fovrt_mod, W, H, scene=scene)
     uni = fovrt_mod.Camera.preset(scene, W, H).uniforms(W, H)
     t.set_camera_uniforms(uni)
@@ -61,13 +60,24 @@ def test_gbuffer_bit_exact(fovrt_mod, oracle, scene):
 # ---------------------------------------------------------------------------------------------
 # entries 1 + 2 — sampling mask (bit-exact), compaction / ray_count (bit-exact)
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("mask_mode", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("scene", [1, 2])
-def test_sampling_and_compaction_bit_exact(fovrt_mod, oracle, scene, mask_mode):
-    W, H = 128, 96
+# (W, H) = (100, 70): partial 16x16 blocks in k_sampling, the ballot publication and k_scatter, as
+# at 1920x1080 (BASELINE configs[1]). gaze_window: a cursor (window coordinates, y down) passed to
+# set_gaze: on the top edge (gaze.y = H) and off the window (k_sampling clamps its focal-depth read).
+SAMPLING_CASES = ([(scene, m, 128, 96, None) for scene in (1, 2) for m in (0, 1, 2, 3, 4)]
+                  + [(1, m, 100, 70, None) for m in (0, 4)]
+                  + [(2, 0, 100, 70, (50.0, 0.0)), (2, 0, 128, 96, (-30.0, 500.0)), (1, 4, 100, 70, (99.5, 0.0)),
+                     (1, 0, 128, 96, (1e6, -1e6))])
+
+
+@pytest.mark.parametrize("scene,mask_mode,W,H,gaze_window", SAMPLING_CASES)
+def test_sampling_and_compaction_bit_exact(fovrt_mod, oracle, scene, mask_mode, W, H, gaze_window):
     t = make_tracer(fovrt_mod, W, H, scene=scene, mask=mask_mode)
     uni = fovrt_mod.Camera.preset(scene, W, H).uniforms(W, H)
     t.set_camera_uniforms(uni)
+    if gaze_window is not None:
+        t.set_gaze(*gaze_window)
+        uni.gaze[0] = np.float32(gaze_window[0])
+        uni.gaze[1] = np.float32(H) - np.float32(gaze_window[1])
     osc = oracle.OracleScene(t.scene_arrays())
     for frame in range(2):  # frame 1 has a valid depth cache -> isValid / reprojection paths
         t.geometry_launch()
@@ -89,15 +99,19 @@ def test_sampling_and_compaction_bit_exact(fovrt_mod, oracle, scene, mask_mode):
         t.shading_launch()
     if mask_mode in (1, 4):
         assert np.array_equal(mask, logpolar_mask_np(W, H, uni.gaze[0], uni.gaze[1], signed=mask_mode == 4))
+    if gaze_window is not None:  # the gaze-target read-back clamps to the screen like the focal-depth read
+        gx = min(max(int(np.float32(uni.gaze[0])), 0), W - 1) if uni.gaze[0] > 0 else 0
+        gy = min(max(int(np.float32(uni.gaze[1])), 0), H - 1) if uni.gaze[1] > 0 else 0
+        assert np.array_equal(np.float32(t.gaze_target()), t.read(TN.POSITION)[gy, gx, :3])
 
 
 # ---------------------------------------------------------------------------------------------
 # entry 3 — foveated shading (north-star tolerance: per-channel RMSE <= 1e-3)
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("scene,spp,dmd,mask_mode", [(0, 1, 1, 3), (1, 1, 1, 1), (1, 4, 3, 1), (1, 4, 3, 3),
-                                                     (2, 2, 3, 0), (2, 8, 1, 1)])
-def test_shading_within_tolerance(fovrt_mod, oracle, scene, spp, dmd, mask_mode):
-    W, H = 64, 48
+@pytest.mark.parametrize("scene,spp,dmd,mask_mode,W,H", [(0, 1, 1, 3, 64, 48), (1, 1, 1, 1, 64, 48), (1, 4, 3, 1, 64, 48),
+                                                         (1, 4, 3, 3, 64, 48), (2, 2, 3, 0, 64, 48), (2, 8, 1, 1, 64, 48),
+                                                         (1, 4, 3, 4, 100, 70)])
+def test_shading_within_tolerance(fovrt_mod, oracle, scene, spp, dmd, mask_mode, W, H):
     t = make_tracer(fovrt_mod, W, H, scene=scene, mask=mask_mode, spp=spp, dmd=dmd)
     uni = fovrt_mod.Camera.preset(scene, W, H).uniforms(W, H)
     t.set_camera_uniforms(uni)
@@ -191,6 +205,7 @@ def test_pullpush_bit_exact_across_frames(fovrt_mod, oracle, W, H):
     rng = np.random.default_rng(W + 7 * H)
     t = _box_tracer(fovrt_mod, W, H)
     st = oracle.PullPushState(W, H)
+    npst = PullPushNp(W, H)  # the independent numpy restatement of the shaders as well
     for k, p in enumerate((0.1, 0.01, 0.3, 0.0)):
         img = sparse_image(W, H, (rng.random((H, W)) < p).astype(np.uint8), seed=k)
         t.write(TN.SHADING, img)
@@ -198,6 +213,7 @@ def test_pullpush_bit_exact_across_frames(fovrt_mod, oracle, W, H):
         got = t.read(TN.PULLPUSH)
         ref = st.render(img)
         assert equal_nan(got, ref), (k, mismatch_report(got, ref))
+        assert equal_nan(got, npst.render(img)), k
 
 
 @pytest.mark.parametrize("count", [1, 2, 3])
@@ -213,6 +229,7 @@ def test_atrous_within_tolerance(fovrt_mod, oracle, count):
     got = t.read(TN.ATROUS)
     ref = oracle.atrous(count, pos, nrm, col)
     assert np.abs(got - ref).max() < 2e-6
+    assert np.abs(got - atrous_np(count, pos, nrm, col)).max() < 4e-6  # the numpy restatement of atFS
 
 
 def test_golden_vectors_on_gpu(fovrt_mod):
@@ -514,3 +531,21 @@ def test_gpu_bvh_follows_moved_triangles(fovrt_mod, oracle):
                       ("diffuse", TN.DIFFUSE)]:
         got = t.read(tid)
         assert equal_nan(got, ref[name]), (name, mismatch_report(got, ref[name]))
+    # the bounding box (depth-saliency theta) follows the geometry; the tree depth is reported
+    flat = pos.reshape(-1, 3)
+    assert np.array_equal(arrays["bbox"], np.concatenate([flat.min(0), flat.max(0)]).astype(np.float32))
+    assert arrays["bvh_depth"] > 0
+    inp = {k: t.read(v) for k, v in [("position", TN.POSITION), ("depth", TN.DEPTH), ("depth_cache", TN.DEPTH_CACHE),
+                                     ("weight", TN.WEIGHT), ("normal", TN.NORMAL), ("diffuse", TN.DIFFUSE)]}
+    t.sampling_launch()
+    sref = oracle.sampling(oracle.OracleScene(arrays), uni, W, H, 1, inp["position"], inp["depth"],
+                           inp["depth_cache"], inp["weight"], inp["normal"], inp["diffuse"])
+    assert np.array_equal(t.read(TN.EXTRA), sref["extra"])
+    # a rejected update leaves the scene as it was
+    bad = pos.copy()
+    bad[0, 0, 0] = np.nan
+    with pytest.raises(RuntimeError):
+        t.set_positions(bad)
+    assert np.array_equal(t.scene_arrays()["pos"].reshape(-1, 3, 3), pos)
+    t.geometry_launch()
+    assert equal_nan(t.read(TN.POSITION), ref["position"])
