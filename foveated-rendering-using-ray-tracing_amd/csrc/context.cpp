@@ -41,6 +41,8 @@ void launch_composite(const f4*, int, int, int, f4*, hipStream_t);
 void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
+void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, int, int, hipStream_t);
+int sibson_prefix_blocks(int W);
 bool gpu_build_bvh(const f3*, int, BvhNode**, TriGeo**, int32_t**, int*, int*, hipStream_t, std::string&);
 #ifdef FR_STAMPS
 void launch_trace_queries(const DevScene&, const f4*, uint32_t, f4*, uint32_t*, hipStream_t, int);
@@ -112,6 +114,7 @@ struct fr_ctx {
   uint32_t* aux_seed = nullptr;   // per active pixel: the seed after the two draws
   u2 *jfa_a = nullptr, *jfa_b = nullptr;  // JFA state ping-pong (seed coord texel + alpha flags)
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
+  f4 *sib_prefix = nullptr, *sib_blocks = nullptr;  // Sibson run form: per-row block prefix sums + block totals
   int pp_S = 0;
   DevStats* stats = nullptr;
   FrameUniforms U;
@@ -423,6 +426,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (cfg.mesh_mode < 0 || cfg.mesh_mode > 2) return fail(nullptr, FR_E_INVALID, "bad mesh_mode");
   if (cfg.scene < 0 || cfg.scene > 2) return fail(nullptr, FR_E_INVALID, "bad scene preset");
   if (cfg.refraction_max_depth < 0 || cfg.refraction_max_depth > 100) return fail(nullptr, FR_E_INVALID, "bad refraction_max_depth");
+  if (cfg.sibson_mode < 0 || cfg.sibson_mode > 1) return fail(nullptr, FR_E_INVALID, "bad sibson_mode");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(nullptr, FR_E_HIP, "no HIP device available");
   if (cfg.device < 0 || cfg.device >= ndev) return fail(nullptr, FR_E_INVALID, "device ordinal out of range");
@@ -527,7 +531,9 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       dalloc(&c->pull, atlas) != hipSuccess || dalloc(&c->push, atlas) != hipSuccess ||
       dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess ||
       dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, N * cfg.spp) != hipSuccess ||
-      dalloc(&c->aux, N) != hipSuccess || dalloc(&c->aux_seed, N) != hipSuccess) {
+      dalloc(&c->aux, N) != hipSuccess || dalloc(&c->aux_seed, N) != hipSuccess ||
+      (cfg.sibson_mode == 0 && (dalloc(&c->sib_prefix, (size_t)(c->W + 1) * c->H) != hipSuccess ||
+                                dalloc(&c->sib_blocks, (size_t)sibson_prefix_blocks(c->W) * c->H) != hipSuccess))) {
     c->err = "device allocation (work buffers) failed";
     return bail(FR_E_NOMEM);
   }
@@ -574,7 +580,7 @@ int fr_destroy(fr_ctx* c) {
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
   fr(c->mask); fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->aux); fr(c->aux_seed); fr(c->jfa_a); fr(c->jfa_b);
-  fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats);
+  fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   for (auto& q : c->kt_ev)
     for (auto e : q) if (e) hipEventDestroy(e);
@@ -750,7 +756,11 @@ static int enqueue_jfa(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {
   return check_launch(c);
 }
 static int enqueue_sibson(fr_ctx* c, hipStream_t stream = nullptr) {
-  launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, stream ? stream : c->stream);
+  if (c->cfg.sibson_mode == 1)  // per tap, bit-exact against the oracle
+    launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, stream ? stream : c->stream);
+  else  // run form (default): exact tap sets, rounding-level differences
+    launch_sibson_runs(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->sib_prefix, c->sib_blocks, c->img[P_SIBSON], c->W,
+                       c->H, stream ? stream : c->stream);
   return check_launch(c);
 }
 static int enqueue_pullpush(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {

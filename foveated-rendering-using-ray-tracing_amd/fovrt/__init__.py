@@ -52,7 +52,8 @@ class fr_config(C.Structure):
                 ("spp", C.c_int), ("diffuse_max_depth", C.c_int), ("refraction_max_depth", C.c_int),
                 ("light_power", C.c_float), ("optimize", C.c_int), ("atrous_iterations", C.c_int),
                 ("write_extra", C.c_int), ("device", C.c_int), ("texture_mode", C.c_int), ("detail", C.c_int),
-                ("mesh_mode", C.c_int), ("bvh_builder", C.c_int), ("asset_dir", C.c_char_p)]
+                ("mesh_mode", C.c_int), ("bvh_builder", C.c_int), ("sibson_mode", C.c_int),
+                ("asset_dir", C.c_char_p)]
 
 
 class fr_camera(C.Structure):
@@ -282,6 +283,7 @@ class Config:
     detail: int = 0
     mesh_mode: int = 0  # 0: .obj meshes where present, else procedural; 1: procedural; 2: .obj required
     bvh_builder: int = 0  # 0: host binned SAH; 1: GPU LBVH (k_bvh.hip)
+    sibson_mode: int = 0  # 0: run form (prefix sums, ~1e-6 of the per-tap sum); 1: per tap, bit-exact
     asset_dir: str = DEFAULT_ASSET_DIR
 
     def to_c(self) -> fr_config:

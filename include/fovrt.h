@@ -69,6 +69,9 @@ typedef struct fr_config {
                                * stand-ins otherwise; 1: procedural only; 2: .obj required (FR_E_IO) */
   int bvh_builder;            /* 0: host binned SAH (default); 1: GPU LBVH (k_bvh.hip), the builder of
                                * fr_rebuild_bvh / fr_set_positions; both give identical frames */
+  int sibson_mode;            /* 0 (default): run form, each row of a pixel's disc summed from per-row prefix
+                               * sums (same taps as sibsonFS.glsl:30-44, rounding-level differences, ~1e-6);
+                               * 1: per tap in the shader's order (bit-exact against the oracle) */
   const char* asset_dir;      /* directory holding CedarCity.hdr, grid.ppm, bunny/bunny.PPM, ... */
 } fr_config;
 

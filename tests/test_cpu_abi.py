@@ -54,7 +54,8 @@ def test_create_without_device_fails_loudly(fovrt_mod):
 @pytest.mark.parametrize("field,value,code", [("spp", 3, "FR_E_UNSUPPORTED"), ("spp", 16, "FR_E_UNSUPPORTED"),
                                               ("spp", 0, "FR_E_UNSUPPORTED"), ("width", 0, "FR_E_INVALID"),
                                               ("mask_mode", 5, "FR_E_INVALID"),
-                                              ("refraction_max_depth", 101, "FR_E_INVALID")])
+                                              ("refraction_max_depth", 101, "FR_E_INVALID"),
+                                              ("sibson_mode", 2, "FR_E_INVALID")])
 def test_create_rejects_bad_config_before_touching_a_device(fovrt_mod, field, value, code):
     """Checked before any HIP call; the megakernel's sample indexing relies on spp in {1, 2, 4, 8}."""
     kw = dict(width=16, height=16, texture_mode=1)

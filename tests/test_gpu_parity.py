@@ -165,8 +165,18 @@ def test_shading_refraction_depth_cap(fovrt_mod, oracle, refr):
 # JumpFlooding / Sibson / PullPush — bit-exact; A-Trous — tolerance
 # ---------------------------------------------------------------------------------------------
 def _box_tracer(fovrt_mod, W, H):
-    return make_tracer(fovrt_mod, W, H, scene=0, mask=3)
+    return make_tracer(fovrt_mod, W, H, scene=0, mask=3, sibson_mode=1)
 
+
+# Sibson run form (sibson_mode 0) against the per-tap form: the taps are the same; a run uses its
+# first tap's 8-bit GL_LINEAR weight for all its taps, and the f32 tap positions of the per-tap form
+# put a weight on the other side of a 1/256 rounding step on a few taps of some rows (the position
+# noise is ~1e-4 texel). One flipped step moves a tap by (1/256) |c1 - c0|, so a pixel's colour by
+# at most 1/256 of a colour difference spread over its taps. Measured at 1080p (10 % log-polar):
+# RMSE 1.35e-5, 99th percentile 1.1e-4, max 6.2e-4. The reference's texture unit rounds its own
+# fixed-point positions, so it is not pinned at this level either.
+SIB_RUN_MAX = 4e-3     # one 1/256 weight step of a full colour difference
+SIB_RUN_RMSE = 5e-5    # per channel; the north-star image tolerance is 1e-3
 
 JFA_CASES = [(64, 48, "logpolar"), (512, 512, "logpolar"), (1920, 1080, "logpolar"), (33, 17, 0.1),
              (40, 40, 0.0), (40, 40, 1.0), (1, 1, 1.0), (7, 5, "single"), (256, 64, 0.003)]
@@ -194,10 +204,41 @@ def test_jfa_and_sibson_bit_exact(fovrt_mod, oracle, W, H, kind):
     assert equal_nan(coord, rc), mismatch_report(coord, rc)
     assert equal_nan(color, rcol), mismatch_report(color, rcol)
     if W * H <= 512 * 512:
+        rs = oracle.sibson(rc, rcol)
+        # sibson_mode 1: per tap, the shader's order -> bit-exact
         fovrt_mod.SibsonInterpolation(t).render()
         si = t.read(TN.SIBSON)
-        rs = oracle.sibson(rc, rcol)
         assert equal_nan(si, rs), mismatch_report(si, rs)
+        # sibson_mode 0 (default): run form over prefix sums -> the same taps, rounding-level differences
+        tf = make_tracer(fovrt_mod, W, H, scene=0, mask=3, sibson_mode=0)
+        tf.write(TN.JFA_COORD, coord)
+        tf.write(TN.JFA_COLOR, color)
+        fovrt_mod.SibsonInterpolation(tf).render()
+        sf = tf.read(TN.SIBSON)
+        assert np.isfinite(sf).all() and np.array_equal(sf[..., 3], rs[..., 3])
+        assert np.abs(sf - rs).max() <= SIB_RUN_MAX, np.abs(sf - rs).max()
+        assert (rmse_per_channel(sf, rs) <= SIB_RUN_RMSE).all(), rmse_per_channel(sf, rs)
+
+
+@pytest.mark.parametrize("W,H", [(1920, 1080), (3840, 2160)])
+def test_sibson_run_form_full_size(fovrt_mod, W, H):
+    """BASELINE sizes (the oracle's per-tap Sibson takes minutes there): the default run form against
+    the per-tap form (bit-exact with the oracle at every size the suite runs it) on the same JFA output
+    of a 10 % log-polar image: same tap sets (alpha, coverage), rounding-level colour differences."""
+    mask = logpolar_mask_np(W, H, W // 2, H - H // 2, signed=True)
+    img = sparse_image(W, H, mask, seed=3)
+    ex = make_tracer(fovrt_mod, W, H, scene=0, mask=3, sibson_mode=1)
+    ru = make_tracer(fovrt_mod, W, H, scene=0, mask=3, sibson_mode=0)
+    ex.write(TN.SHADING, img)
+    fovrt_mod.JumpFlooding(ex).render(TN.SHADING)
+    fovrt_mod.SibsonInterpolation(ex).render()
+    ru.write(TN.JFA_COORD, ex.read(TN.JFA_COORD))
+    ru.write(TN.JFA_COLOR, ex.read(TN.JFA_COLOR))
+    fovrt_mod.SibsonInterpolation(ru).render()
+    a, b = ex.read(TN.SIBSON), ru.read(TN.SIBSON)
+    assert np.isfinite(b).all() and np.array_equal(a[..., 3], b[..., 3])
+    assert np.abs(a - b).max() <= SIB_RUN_MAX, np.abs(a - b).max()
+    assert (rmse_per_channel(a, b) <= SIB_RUN_RMSE).all(), rmse_per_channel(a, b)
 
 
 @pytest.mark.parametrize("W,H", [(64, 64), (96, 64), (256, 256), (130, 70)])
