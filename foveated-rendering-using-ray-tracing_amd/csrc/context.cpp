@@ -39,7 +39,7 @@ void launch_shard_pack(const FrameUniforms&, const f4*, f4*, hipStream_t);
 void launch_logpolar(const f4*, f4*, f4*, int, int, f2, hipStream_t);
 void launch_composite(const f4*, int, int, int, f4*, hipStream_t);
 void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
-void launch_jfa(const f4*, u2*, u2*, f4*, f4*, int, int, hipStream_t);
+void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
 void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, int, int, hipStream_t);
 int sibson_prefix_blocks(int W);
@@ -113,6 +113,7 @@ struct fr_ctx {
   f4* aux = nullptr;              // per active pixel: NDC position, r1, r2 (k_sample_setup)
   uint32_t* aux_seed = nullptr;   // per active pixel: the seed after the two draws
   u2 *jfa_a = nullptr, *jfa_b = nullptr;  // JFA state ping-pong (seed coord texel + alpha flags)
+  float* ftab = nullptr;  // texel-centre coordinates ((x + 0.5) / W, x < W; then (y + 0.5) / H)
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
   f4 *sib_prefix = nullptr, *sib_blocks = nullptr;  // Sibson run form: per-row block prefix sums + block totals
   int pp_S = 0;
@@ -537,6 +538,12 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     c->err = "device allocation (work buffers) failed";
     return bail(FR_E_NOMEM);
   }
+  {  // texel centres in texture coordinates, IEEE-correctly-rounded division as in the kernels
+    std::vector<float> ft((size_t)c->W + c->H);
+    for (int x = 0; x < c->W; x++) ft[x] = ((float)x + 0.5f) / (float)c->W;
+    for (int y = 0; y < c->H; y++) ft[(size_t)c->W + y] = ((float)y + 0.5f) / (float)c->H;
+    if (!up(&c->ftab, ft)) { c->err = "device allocation (work buffers) failed"; return bail(FR_E_NOMEM); }
+  }
   // Default camera: the preset pose, prev = current.
   FrameUniforms& U = c->U;
   memset(&U, 0, sizeof(U));
@@ -579,7 +586,7 @@ int fr_destroy(fr_ctx* c) {
   for (auto p : c->d_tex) fr(p);
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
-  fr(c->mask); fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->aux); fr(c->aux_seed); fr(c->jfa_a); fr(c->jfa_b);
+  fr(c->mask); fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->aux); fr(c->aux_seed); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   for (auto& q : c->kt_ev)
@@ -751,7 +758,7 @@ static int resolve(fr_ctx* c, int id, int* phys) {
 static int enqueue_jfa(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {
   int p;
   if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "jfa: bad input buffer");
-  launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->W, c->H,
+  launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->ftab, c->W, c->H,
              stream ? stream : c->stream);
   return check_launch(c);
 }
