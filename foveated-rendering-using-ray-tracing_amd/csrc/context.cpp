@@ -62,7 +62,10 @@ static thread_local std::string g_create_error;
 enum Phys {
   P_POSITION, P_NORMAL, P_DEPTH_A, P_DEPTH_B, P_DIFFUSE, P_WEIGHT, P_HIST_A, P_HIST_B, P_SHADING, P_EXTRA,
   P_JFA_COORD, P_JFA_COLOR, P_SIBSON, P_PULLPUSH, P_ATROUS_A, P_ATROUS_B, P_LOGPOLAR, P_LOGPOLAR_INV,
-  P_POSITION_B, P_NORMAL_B, P_SHADING_B,  // frame-parity partners of the buffers the reconstruction reads
+  // frame-slot copies of the buffers the reconstruction reads (POSITION, NORMAL, SHADING) and of
+  // WEIGHT (read by the trace half's tail); slot 0 is the plain entry above
+  P_POSITION_B, P_NORMAL_B, P_SHADING_B, P_WEIGHT_B,
+  P_POSITION_C, P_NORMAL_C, P_SHADING_C, P_WEIGHT_C,
   P_COUNT
 };
 
@@ -75,11 +78,25 @@ struct fr_ctx {
   hipStream_t stream2 = nullptr;  // reconstruction chain 2: pull-push -> A-Trous
   hipStream_t stream3 = nullptr;  // reconstruction chain 1: JFA -> Sibson
   hipStream_t stream4 = nullptr;  // entry 3's carry of the inactive pixels, beside the megakernel
-  // Frame pipelining: frame N's reconstruction (stream3 + stream2) runs while frame N+1 traces on
-  // `stream`. The buffers the reconstruction reads (POSITION, NORMAL, SHADING) alternate by frame
-  // parity `par`; the trace half of a frame waits for the reconstruction that last read its parity.
-  int par = 0;
-  bool recon_pending[2] = {false, false};
+  hipStream_t stream5 = nullptr;  // front stages of a pipelined frame (entries 0-2), beside the previous megakernel
+  // Frame pipelining: frame N's reconstruction (stream3 + stream2) runs while later frames trace.
+  // The buffers the reconstruction reads (POSITION, NORMAL, SHADING) rotate over `nslots` frame
+  // slots (`slot` = the current frame's); a frame's front stages wait for the reconstruction that
+  // last read their slot (ev_recon). The front stages of a pipelined frame (G-buffer, sampling,
+  // compaction) run on stream5 while the previous frame's megakernel still runs on `stream`: they
+  // read nothing entry 3 writes. What entry 3's tail reads of them (WEIGHT, mask, active list, ray
+  // count) rotates with the slot as well; the front of a frame waits for the trace half that last
+  // read its slot (ev_trace), and entry 3 of a frame waits for its own front (ev_front).
+  static constexpr int MAX_SLOTS = 3;
+  int nslots = 3;
+  int slot = 0;
+  bool recon_pending[MAX_SLOTS] = {};
+  bool front_pending = false;
+  bool trace_pending[MAX_SLOTS] = {};
+  hipEvent_t ev_front = nullptr, ev_trace[MAX_SLOTS] = {}, ev_recon[MAX_SLOTS] = {};
+  uint8_t* mask_p[MAX_SLOTS] = {};
+  uint32_t* active_p[MAX_SLOTS] = {};
+  uint32_t* ray_count_p[MAX_SLOTS] = {};
   HostScene scene;
   Bvh bvh;
   // device scene
@@ -97,7 +114,7 @@ struct fr_ctx {
   int depth_cur = P_DEPTH_A, depth_cache = P_DEPTH_B;
   int hist_cur = P_HIST_A, hist_cache = P_HIST_B;
   int atrous_out = P_ATROUS_A;
-  uint8_t* mask = nullptr;
+  uint8_t* mask = nullptr;  // mask_p[slot]
   uint8_t* gclass = nullptr;
   uint8_t* lp_cache = nullptr;  // log-polar mask for (lp_gaze, lp_mode); recomputed when either changes
   f2 lp_gaze{-1e30f, -1e30f};
@@ -106,8 +123,8 @@ struct fr_ctx {
   uint32_t* counts = nullptr;
   uint32_t* offsets = nullptr;  // per (class, block) local prefix
   uint32_t* tiles = nullptr;
-  uint32_t* ray_count = nullptr;
-  uint32_t* active = nullptr;
+  uint32_t* ray_count = nullptr;  // ray_count_p[slot]
+  uint32_t* active = nullptr;     // active_p[slot]
   uint32_t* shade_ctr = nullptr;  // sharded chunk counters of the shading work queue
   f4* samples = nullptr;          // one radiance value per (active pixel, camera sample)
   f4* aux = nullptr;              // per active pixel: NDC position, r1, r2 (k_sample_setup)
@@ -123,8 +140,7 @@ struct fr_ctx {
   bool light_pending = false;
   bool compacted = false;
   bool mask_dirty = false;
-  hipEvent_t ev[24] = {};  // 0-15 stage timing; 16 fork; 17 chain-2 join; 18, 19 reconstruction done per parity;
-                           // 20-22 chain-1 timing
+  hipEvent_t ev[24] = {};  // 0-15 stage timing; 16 fork; 17 chain-2 join; 20-22 chain-1 timing
   bool time_kernels = false;  // fr_frame with timing: also time the path-trace kernel alone
   // Live timing of entry 3 inside pipelined (untimed) frames: a ring of event quadruples recorded on
   // the context stream around carry_history / k_shade_paths / resolve (fr_kernel_timing); a slot is
@@ -450,11 +466,19 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_lo) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, prio_hi) != hipSuccess) {
     c->err = "stream create failed";
     return bail(FR_E_HIP);
   }
   for (auto& e : c->ev) hipEventCreate(&e);
+  hipEventCreateWithFlags(&c->ev_front, hipEventDisableTiming);
+  for (auto& e : c->ev_trace) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& e : c->ev_recon) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  {  // FOVRT_SLOTS: frame slots of the pipelined loop (2 or 3; A/B knob)
+    const char* v = getenv("FOVRT_SLOTS");
+    if (v) c->nslots = std::max(2, std::min(fr_ctx::MAX_SLOTS, atoi(v)));
+  }
 
   std::string err;
   if (!build_preset_scene(cfg.scene, c->asset_dir, cfg.texture_mode, cfg.light_power, cfg.detail, c->scene, err,
@@ -525,10 +549,16 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   c->pp_S = pp_size(c->W, c->H);
   const size_t atlas = (size_t)c->pp_S * (c->pp_S + c->pp_S / 2);
   if (compaction_tiles(c->W, c->H) > 1024) { c->err = "screen too large for the compaction scan"; return bail(FR_E_UNSUPPORTED); }
-  if (dalloc(&c->mask, N) != hipSuccess || dalloc(&c->gclass, N) != hipSuccess || dalloc(&c->lp_cache, N) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
+  for (int k = 0; k < c->nslots; k++)
+    if (dalloc(&c->mask_p[k], N) != hipSuccess || dalloc(&c->ray_count_p[k], 4) != hipSuccess ||
+        dalloc(&c->active_p[k], N) != hipSuccess) {
+      c->err = "device allocation (work buffers) failed";
+      return bail(FR_E_NOMEM);
+    }
+  c->mask = c->mask_p[0]; c->ray_count = c->ray_count_p[0]; c->active = c->active_p[0];
+  if (dalloc(&c->gclass, N) != hipSuccess || dalloc(&c->lp_cache, N) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
       dalloc(&c->counts, 4 * nblocks) != hipSuccess || dalloc(&c->offsets, 4 * nblocks) != hipSuccess ||
-      dalloc(&c->tiles, 1024) != hipSuccess || dalloc(&c->ray_count, 4) != hipSuccess ||
-      dalloc(&c->active, N) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
+      dalloc(&c->tiles, 1024) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
       dalloc(&c->pull, atlas) != hipSuccess || dalloc(&c->push, atlas) != hipSuccess ||
       dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess ||
       dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, N * cfg.spp) != hipSuccess ||
@@ -581,20 +611,26 @@ int fr_destroy(fr_ctx* c) {
   if (c->stream2) hipStreamSynchronize(c->stream2);
   if (c->stream3) hipStreamSynchronize(c->stream3);
   if (c->stream4) hipStreamSynchronize(c->stream4);
+  if (c->stream5) hipStreamSynchronize(c->stream5);
   auto fr = [](void* p) { if (p) hipFree(p); };
   fr(c->d_nodes); fr(c->d_tri); fr(c->d_prim); fr(c->d_shade); fr(c->d_pos);
   for (auto p : c->d_tex) fr(p);
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
-  fr(c->mask); fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->ray_count); fr(c->active); fr(c->shade_ctr); fr(c->samples); fr(c->aux); fr(c->aux_seed); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
+  for (int k = 0; k < fr_ctx::MAX_SLOTS; k++) { fr(c->mask_p[k]); fr(c->ray_count_p[k]); fr(c->active_p[k]); }
+  fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->aux); fr(c->aux_seed); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
+  if (c->ev_front) hipEventDestroy(c->ev_front);
+  for (auto e : c->ev_trace) if (e) hipEventDestroy(e);
+  for (auto e : c->ev_recon) if (e) hipEventDestroy(e);
   for (auto& q : c->kt_ev)
     for (auto e : q) if (e) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream3) hipStreamDestroy(c->stream3);
   if (c->stream4) hipStreamDestroy(c->stream4);
+  if (c->stream5) hipStreamDestroy(c->stream5);
   delete c;
   return FR_OK;
 }
@@ -636,23 +672,33 @@ int fr_accum_frame(fr_ctx* c, uint32_t* f) {
   return FR_OK;
 }
 
-static int P_pos(const fr_ctx* c) { return c->par ? P_POSITION_B : P_POSITION; }
-static int P_nrm(const fr_ctx* c) { return c->par ? P_NORMAL_B : P_NORMAL; }
-static int P_shd(const fr_ctx* c) { return c->par ? P_SHADING_B : P_SHADING; }
+static int slotted(const fr_ctx* c, int p0, int pb) { return c->slot == 0 ? p0 : pb + 4 * (c->slot - 1); }
+static int P_pos(const fr_ctx* c) { return slotted(c, P_POSITION, P_POSITION_B); }
+static int P_nrm(const fr_ctx* c) { return slotted(c, P_NORMAL, P_NORMAL_B); }
+static int P_shd(const fr_ctx* c) { return slotted(c, P_SHADING, P_SHADING_B); }
+static int P_wgt(const fr_ctx* c) { return slotted(c, P_WEIGHT, P_WEIGHT_B); }
 
 // The context stream waits for every reconstruction still in flight (before any call that reads or
 // writes what the reconstruction uses, or hands buffers to the caller).
 static void join_recon(fr_ctx* c) {
-  for (int k = 0; k < 2; k++)
-    if (c->recon_pending[k]) { hipStreamWaitEvent(c->stream, c->ev[18 + k], 0); c->recon_pending[k] = false; }
+  for (int k = 0; k < fr_ctx::MAX_SLOTS; k++)
+    if (c->recon_pending[k]) { hipStreamWaitEvent(c->stream, c->ev_recon[k], 0); c->recon_pending[k] = false; }
+  if (c->front_pending) { hipStreamWaitEvent(c->stream, c->ev_front, 0); c->front_pending = false; }
 }
 
-static int enqueue_geometry(fr_ctx* c) {
-  // a new frame: switch to the other parity, once the reconstruction that read it has finished
-  c->par ^= 1;
-  if (c->recon_pending[c->par]) {
-    hipStreamWaitEvent(c->stream, c->ev[18 + c->par], 0);
-    c->recon_pending[c->par] = false;
+// fs: the stream of the front stages (entries 0-2): `stream`, or stream5 in a pipelined frame.
+static int enqueue_geometry(fr_ctx* c, hipStream_t fs) {
+  // a new frame: move to the next slot, once the reconstruction that read it has finished
+  c->slot = (c->slot + 1) % c->nslots;
+  const int sl = c->slot;
+  c->mask = c->mask_p[sl]; c->active = c->active_p[sl]; c->ray_count = c->ray_count_p[sl];
+  if (c->recon_pending[sl]) {
+    hipStreamWaitEvent(fs, c->ev_recon[sl], 0);  // entry 3 on `stream` waits for fs (ev_front)
+    c->recon_pending[sl] = false;
+  }
+  if (fs != c->stream && c->trace_pending[sl]) {
+    hipStreamWaitEvent(fs, c->ev_trace[sl], 0);
+    c->trace_pending[sl] = false;
   }
   // frame = m_accumFrame++ ; a light change resets the counter afterwards (FR/PathTracer.cpp:99-116)
   c->U.frame = c->accum++;
@@ -663,38 +709,42 @@ static int enqueue_geometry(fr_ctx* c) {
     hipMemsetAsync(c->img[c->hist_cache], 0, bytes, c->stream);
   }
   launch_gbuffer(c->dsc, c->U, c->img[P_pos(c)], c->img[P_nrm(c)], c->img[c->depth_cur], c->img[P_DIFFUSE],
-                 c->img[P_WEIGHT], c->gclass, c->stats, c->stream);
+                 c->img[P_wgt(c)], c->gclass, c->stats, fs);
   c->compacted = false;
   return check_launch(c);
 }
 
-static int enqueue_sampling(fr_ctx* c) {
+static int enqueue_sampling(fr_ctx* c, hipStream_t fs) {
   c->mask_dirty = false;
   const bool lp = c->U.mask_mode == FR_MASK_LOGPOLAR || c->U.mask_mode == FR_MASK_LOGPOLAR_SIGNED;
   const bool lp_refresh = lp && (c->lp_mode != c->U.mask_mode || c->lp_gaze.x != c->U.gaze.x ||
                                  c->lp_gaze.y != c->U.gaze.y);
   if (lp_refresh) { c->lp_mode = c->U.mask_mode; c->lp_gaze = c->U.gaze; }
-  launch_sampling(c->U, c->dsc, c->img[P_pos(c)], c->img[c->depth_cur], c->img[c->depth_cache], c->img[P_WEIGHT],
+  launch_sampling(c->U, c->dsc, c->img[P_pos(c)], c->img[c->depth_cur], c->img[c->depth_cache], c->img[P_wgt(c)],
                   c->img[P_nrm(c)], c->img[P_DIFFUSE], c->img[P_EXTRA], c->mask, c->gclass, c->words, c->counts,
-                  c->cfg.write_extra, c->lp_cache, lp_refresh, c->stream);
+                  c->cfg.write_extra, c->lp_cache, lp_refresh, fs);
   c->compacted = false;
   return check_launch(c);
 }
 
-static int enqueue_optimize(fr_ctx* c) {
+static int enqueue_optimize(fr_ctx* c, hipStream_t fs) {
   if (c->mask_dirty) {
-    launch_mask_words(c->mask, c->gclass, c->W, c->H, c->words, c->counts, c->stream);
+    launch_mask_words(c->mask, c->gclass, c->W, c->H, c->words, c->counts, fs);
     c->mask_dirty = false;
   }
-  launch_compaction(c->W, c->H, c->words, c->counts, c->offsets, c->tiles, c->ray_count, c->active, c->stream);
+  launch_compaction(c->W, c->H, c->words, c->counts, c->offsets, c->tiles, c->ray_count, c->active, fs);
   c->compacted = true;
   return check_launch(c);
 }
 
 static int enqueue_shading(fr_ctx* c) {
   if (!c->compacted) {  // g_isOptimize = 0: the active list is still needed by this design
-    int rc = enqueue_optimize(c);
+    int rc = enqueue_optimize(c, c->stream);
     if (rc) return rc;
+  }
+  if (c->front_pending) {  // a pipelined frame: entry 3 waits for its own front stages
+    hipStreamWaitEvent(c->stream, c->ev_front, 0);
+    c->front_pending = false;
   }
   hipEvent_t* kt = nullptr;
   if (c->kt_on) {
@@ -709,22 +759,25 @@ static int enqueue_shading(fr_ctx* c) {
   // it runs on stream4 beside the latency-bound megakernel and joins before the resolve.
   hipEventRecord(c->ev[11], c->stream);
   hipStreamWaitEvent(c->stream4, c->ev[11], 0);
-  launch_carry_history(c->U, c->mask, c->img[P_WEIGHT], c->img[c->hist_cache], c->img[c->hist_cur],
+  launch_carry_history(c->U, c->mask, c->img[P_wgt(c)], c->img[c->hist_cache], c->img[c->hist_cur],
                        c->img[P_shd(c)], c->stream4);
   hipEventRecord(c->ev[12], c->stream4);
   const uint32_t N = (uint32_t)((size_t)c->W * c->H);
-  launch_sample_setup(c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache], c->aux, c->aux_seed,
+  launch_sample_setup(c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache], c->aux, c->aux_seed,
                       c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
   if (kt) hipEventRecord(kt[1], c->stream);
-  launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache],
+  launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache],
                      c->shade_ctr, c->samples, c->stats, c->aux, c->aux_seed, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   if (kt) hipEventRecord(kt[2], c->stream);
   hipStreamWaitEvent(c->stream, c->ev[12], 0);
-  launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_WEIGHT], c->img[c->hist_cache], c->samples,
+  launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache], c->samples,
                        c->img[c->hist_cur], c->img[P_shd(c)], c->shade_ctr, c->stream);
   if (kt) hipEventRecord(kt[3], c->stream);
+  // this slot's WEIGHT / mask / active list are free for the front stages of frame + nslots after this
+  hipEventRecord(c->ev_trace[c->slot], c->stream);
+  c->trace_pending[c->slot] = true;
   int rc = check_launch(c);
   // swapBuffer("history_cache", "history_buffer"); swapBuffer("depth_cache", "depth_buffer") (:226-227)
   std::swap(c->hist_cur, c->hist_cache);
@@ -739,7 +792,7 @@ static int resolve(fr_ctx* c, int id, int* phys) {
     case FR_BUF_DEPTH: *phys = c->depth_cur; return FR_OK;
     case FR_BUF_DEPTH_CACHE: *phys = c->depth_cache; return FR_OK;
     case FR_BUF_DIFFUSE: *phys = P_DIFFUSE; return FR_OK;
-    case FR_BUF_WEIGHT: *phys = P_WEIGHT; return FR_OK;
+    case FR_BUF_WEIGHT: *phys = P_wgt(c); return FR_OK;
     case FR_BUF_HISTORY: *phys = c->hist_cur; return FR_OK;
     case FR_BUF_HISTORY_CACHE: *phys = c->hist_cache; return FR_OK;
     case FR_BUF_SHADING: *phys = P_shd(c); return FR_OK;
@@ -809,9 +862,9 @@ static int timed(fr_ctx* c, const std::function<int()>& f, float* ms) {
   return FR_OK;
 }
 
-int fr_geometry_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_geometry(c); }, ms); }
-int fr_sampling_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_sampling(c); }, ms); }
-int fr_optimize_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_optimize(c); }, ms); }
+int fr_geometry_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_geometry(c, c->stream); }, ms); }
+int fr_sampling_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_sampling(c, c->stream); }, ms); }
+int fr_optimize_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_optimize(c, c->stream); }, ms); }
 int fr_shading_launch(fr_ctx* c, float* ms) { if (!c) return FR_E_INVALID; return timed(c, [&] { return enqueue_shading(c); }, ms); }
 
 static int ns_timed(fr_ctx* c, std::function<int()> f, uint64_t* ns) {
@@ -884,12 +937,19 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
   int rc;
   if (t) hipEventRecord(ev[0], c->stream);
   if (trace) {
-    if ((rc = enqueue_geometry(c))) return rc;
+    // untimed frames pipeline: the front stages go to stream5 and overlap the previous frame's
+    // entry 3 (timed frames keep every stage on `stream`, one after the other)
+    hipStream_t fs = t ? c->stream : c->stream5;
+    if ((rc = enqueue_geometry(c, fs))) return rc;
     if (t) hipEventRecord(ev[1], c->stream);
-    if ((rc = enqueue_sampling(c))) return rc;
+    if ((rc = enqueue_sampling(c, fs))) return rc;
     if (t) hipEventRecord(ev[2], c->stream);
-    if ((rc = enqueue_optimize(c))) return rc;
+    if ((rc = enqueue_optimize(c, fs))) return rc;
     if (t) hipEventRecord(ev[3], c->stream);
+    if (!t) {
+      hipEventRecord(c->ev_front, fs);
+      c->front_pending = true;
+    }
     c->time_kernels = t != nullptr;
     rc = enqueue_shading(c);
     c->time_kernels = false;
@@ -904,7 +964,7 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     // The reconstruction of this frame's shading runs on its own streams, so the next frame's trace
     // half (on `stream`) overlaps it. Two independent chains read the shading: JFA -> Sibson
     // (stream3) and pull-push -> A-Trous (stream2; atFS binds the JFA texture but never reads it,
-    // FR/shader/atFS.glsl:40-90). Both resolve their inputs now, at this frame's parity.
+    // FR/shader/atFS.glsl:40-90). Both resolve their inputs now, at this frame's slot.
     hipEventRecord(ev[16], c->stream);
     hipStreamWaitEvent(c->stream3, ev[16], 0);
     hipStreamWaitEvent(c->stream2, ev[16], 0);
@@ -921,8 +981,8 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     if (t) hipEventRecord(ev[15], c->stream2);
     hipEventRecord(ev[17], c->stream2);
     hipStreamWaitEvent(c->stream3, ev[17], 0);
-    hipEventRecord(ev[18 + c->par], c->stream3);  // this parity's buffers are free again after this
-    c->recon_pending[c->par] = true;
+    hipEventRecord(c->ev_recon[c->slot], c->stream3);  // this slot's buffers are free again after this
+    c->recon_pending[c->slot] = true;
     if (t) join_recon(c);
   }
   if (t) {
