@@ -455,19 +455,23 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   c->W = cfg.width; c->H = cfg.height;
   auto bail = [&](int code) { g_create_error = c->err; fr_destroy(c); return code; };
   if (hipSetDevice(cfg.device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(FR_E_HIP); }
-  // The trace half (context stream) is the frame's critical path; the reconstruction streams have a
-  // frame of slack (FOVRT_STREAM_PRIORITY=0: all streams at the default priority).
-  int prio_lo = 0, prio_hi = 0;
-  static const bool use_prio = [] {
+  // Stream priorities (FOVRT_STREAM_PRIORITY, A/B knob): 0 (default) all streams at the default
+  // priority; 1 trace half (context stream, carry, front stages) high, reconstruction low; 2 the
+  // reconstruction high, the trace half low; 3 only the front stages high.
+  static const int prio_mode = [] {
     const char* v = getenv("FOVRT_STREAM_PRIORITY");
-    return !v || atoi(v) != 0;
+    return v ? atoi(v) : 0;
   }();
-  if (use_prio) hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_lo) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+  int lo = 0, hi = 0;
+  if (prio_mode) hipDeviceGetStreamPriorityRange(&lo, &hi);
+  const int p_trace = prio_mode == 1 ? hi : prio_mode == 2 ? lo : 0;
+  const int p_recon = prio_mode == 1 ? lo : prio_mode == 2 ? hi : 0;
+  const int p_front = prio_mode == 1 || prio_mode == 3 ? hi : prio_mode == 2 ? lo : 0;
+  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, p_trace) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, p_recon) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, p_recon) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, p_trace) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, p_front) != hipSuccess) {
     c->err = "stream create failed";
     return bail(FR_E_HIP);
   }
@@ -1215,6 +1219,12 @@ extern "C" int fr_diag_trace_queries(fr_ctx* c, float* out) {
       if ((d[2 * (size_t)i + 1].w != 0.0f) == (pass == 1)) { part.push_back(d[2 * (size_t)i]); part.push_back(d[2 * (size_t)i + 1]); }
   size_t shadow = 0;
   for (uint32_t i = 0; i < n; i++) shadow += d[2 * (size_t)i + 1].w != 0.0f;
+  if (const char* path = getenv("FOVRT_DIAG_DUMP")) {  // every 16th query (o, tmax, d, any) for offline BVH studies
+    if (FILE* f = fopen(path, "wb")) {
+      for (uint32_t i = 0; i < n; i += 16) fwrite(&d[2 * (size_t)i], sizeof(f4), 2, f);
+      fclose(f);
+    }
+  }
   const uint32_t nc = n - (uint32_t)shadow;
   HIP_TRY(c, hipMemcpy(rec, part.data(), (size_t)n * 32, hipMemcpyHostToDevice));
   const float t_sorted = timeit([&] { launch_trace_queries(c->dsc, rec, n, hits, ctr, c->stream, 0); });
