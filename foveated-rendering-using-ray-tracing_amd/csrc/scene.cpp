@@ -656,9 +656,74 @@ struct Builder {
   Bvh& out;
   static constexpr int kMaxBins = 64, kMaxDepth = 30;
   int kLeaf = 2, kBins = 16;  // leaf size and SAH bins (FOVRT_BVH_LEAF / FOVRT_BVH_BINS override, for tuning)
+  int kSplit = 0;             // FOVRT_BVH_SPLIT: 0 binned on the widest centroid axis; 1 binned on all three
+                              // axes; 2 exact sweep over the sorted centroids of all three axes
   Builder(const HostScene& sc, Bvh& o) : s(sc), out(o) {
     if (const char* v = getenv("FOVRT_BVH_LEAF")) kLeaf = std::max(1, std::min(8, atoi(v)));
     if (const char* v = getenv("FOVRT_BVH_BINS")) kBins = std::max(2, std::min(kMaxBins, atoi(v)));
+    if (const char* v = getenv("FOVRT_BVH_SPLIT")) kSplit = std::max(0, std::min(2, atoi(v)));
+  }
+  static float axis_of(f3 c, int a) { return a == 0 ? c.x : a == 1 ? c.y : c.z; }
+  // Exact SAH sweep on all three axes: sorts [b, e) by the best axis and returns the split point.
+  int split_sweep(int b, int e) {
+    const int n = e - b;
+    std::vector<float> right(n);
+    float best = INFINITY;
+    int best_axis = -1, best_i = -1;
+    std::vector<int32_t> tmp(ids.begin() + b, ids.begin() + e);
+    for (int a = 0; a < 3; a++) {
+      std::sort(tmp.begin(), tmp.end(), [&](int x, int y) {
+        const float kx = axis_of(cen[x], a), ky = axis_of(cen[y], a);
+        return kx < ky || (kx == ky && x < y);
+      });
+      Box r;
+      for (int i = n - 1; i >= 1; i--) { r.grow(tb[tmp[i]]); right[i] = r.area(); }
+      Box l;
+      for (int i = 1; i < n; i++) {
+        l.grow(tb[tmp[i - 1]]);
+        const float c = l.area() * i + right[i] * (n - i);
+        if (c < best) { best = c; best_axis = a; best_i = i; }
+      }
+    }
+    if (best_axis < 0) return -1;
+    std::sort(ids.begin() + b, ids.begin() + e, [&](int x, int y) {
+      const float kx = axis_of(cen[x], best_axis), ky = axis_of(cen[y], best_axis);
+      return kx < ky || (kx == ky && x < y);
+    });
+    return b + best_i;
+  }
+  // Binned SAH on all three axes.
+  int split_binned3(int b, int e, const Box& cb) {
+    float best = INFINITY;
+    int best_axis = -1, best_k = -1;
+    for (int a = 0; a < 3; a++) {
+      const float lo = axis_of(cb.lo, a), ex = axis_of(cb.hi, a) - lo;
+      if (!(ex > 0.0f)) continue;
+      Box bins[kMaxBins];
+      int cnt[kMaxBins] = {0};
+      for (int i = b; i < e; i++) {
+        int k = (int)((axis_of(cen[ids[i]], a) - lo) / ex * kBins);
+        k = k < 0 ? 0 : (k >= kBins ? kBins - 1 : k);
+        cnt[k]++; bins[k].grow(tb[ids[i]]);
+      }
+      float ra[kMaxBins]; int rn[kMaxBins];
+      Box r; int nr = 0;
+      for (int k = kBins - 1; k >= 1; k--) { if (cnt[k]) { r.grow(bins[k]); nr += cnt[k]; } ra[k] = r.area(); rn[k] = nr; }
+      Box l; int nl = 0;
+      for (int k = 1; k < kBins; k++) {
+        if (cnt[k - 1]) { l.grow(bins[k - 1]); nl += cnt[k - 1]; }
+        if (!nl || !rn[k]) continue;
+        const float c = l.area() * nl + ra[k] * rn[k];
+        if (c < best) { best = c; best_axis = a; best_k = k; }
+      }
+    }
+    if (best_axis < 0) return -1;
+    const float lo = axis_of(cb.lo, best_axis), ex = axis_of(cb.hi, best_axis) - lo;
+    return (int)(std::partition(ids.begin() + b, ids.begin() + e, [&](int id) {
+             int k = (int)((axis_of(cen[id], best_axis) - lo) / ex * kBins);
+             k = k < 0 ? 0 : (k >= kBins ? kBins - 1 : k);
+             return k < best_k;
+           }) - ids.begin());
   }
 
   Box range_box(int b, int e) const { Box bx; for (int i = b; i < e; i++) bx.grow(tb[ids[i]]); return bx; }
@@ -680,7 +745,11 @@ struct Builder {
     float ex = axis == 0 ? ext.x : axis == 1 ? ext.y : ext.z;
     auto key = [&](int id) { f3 c = cen[id]; return axis == 0 ? c.x : axis == 1 ? c.y : c.z; };
     int mid = -1;
-    if (ex > 0.0f) {
+    if (kSplit == 2) {
+      mid = split_sweep(b, e);
+    } else if (kSplit == 1) {
+      mid = split_binned3(b, e, cb);
+    } else if (ex > 0.0f) {
       Box bins[kMaxBins];
       int cnt[kMaxBins] = {0};
       auto bin_of = [&](int id) { int k = (int)((key(id) - lo) / ex * kBins); return k < 0 ? 0 : (k >= kBins ? kBins - 1 : k); };

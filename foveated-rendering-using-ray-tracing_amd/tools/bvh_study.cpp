@@ -124,6 +124,152 @@ struct Sim {
   }
 };
 
+// ---- generic-width study tree: the engine's binned SAH binary build, collapsed to `width` children
+// per node (largest-area inner entry opened first), leaf children in one contiguous triangle range.
+struct GBox {
+  f3 lo = mk3(INFINITY), hi = mk3(-INFINITY);
+  void grow(f3 p) { lo = mk3(fminf(lo.x, p.x), fminf(lo.y, p.y), fminf(lo.z, p.z)); hi = mk3(fmaxf(hi.x, p.x), fmaxf(hi.y, p.y), fmaxf(hi.z, p.z)); }
+  void grow(const GBox& b) { grow(b.lo); grow(b.hi); }
+  float area() const { f3 d = hi - lo; return d.x < 0 ? 0.0f : 2.0f * (d.x * d.y + d.y * d.z + d.z * d.x); }
+};
+struct GNode { std::vector<GBox> box; std::vector<int> child, count; };
+struct GTree {
+  std::vector<GNode> nodes;
+  std::vector<int> prim;  // leaf order
+};
+struct GBuilder {
+  const HostScene& s;
+  int width, leaf = 2, bins = 16;
+  std::vector<GBox> tb; std::vector<f3> cen; std::vector<int> ids;
+  struct B2 { GBox box[2]; int child[2], count[2]; };
+  std::vector<B2> bin;
+  std::vector<int> lprim;
+  GTree out;
+  int split(int b, int e) {
+    const int n = e - b;
+    if (n <= leaf) return -1;
+    GBox cb; for (int i = b; i < e; i++) cb.grow(cen[ids[i]]);
+    f3 ext = cb.hi - cb.lo;
+    int axis = ext.x > ext.y ? (ext.x > ext.z ? 0 : 2) : (ext.y > ext.z ? 1 : 2);
+    auto key = [&](int id) { f3 c = cen[id]; return axis == 0 ? c.x : axis == 1 ? c.y : c.z; };
+    const float lo = axis == 0 ? cb.lo.x : axis == 1 ? cb.lo.y : cb.lo.z, ex = axis == 0 ? ext.x : axis == 1 ? ext.y : ext.z;
+    int mid = -1;
+    if (ex > 0) {
+      GBox bx[64]; int cnt[64] = {0};
+      auto bof = [&](int id) { int k = (int)((key(id) - lo) / ex * bins); return k < 0 ? 0 : k >= bins ? bins - 1 : k; };
+      for (int i = b; i < e; i++) { int k = bof(ids[i]); cnt[k]++; bx[k].grow(tb[ids[i]]); }
+      float best = INFINITY; int bk = -1;
+      for (int k = 1; k < bins; k++) {
+        GBox l, r; int nl = 0, nr = 0;
+        for (int j = 0; j < k; j++) if (cnt[j]) { l.grow(bx[j]); nl += cnt[j]; }
+        for (int j = k; j < bins; j++) if (cnt[j]) { r.grow(bx[j]); nr += cnt[j]; }
+        if (!nl || !nr) continue;
+        float c = l.area() * nl + r.area() * nr;
+        if (c < best) { best = c; bk = k; }
+      }
+      if (bk > 0) mid = (int)(std::partition(ids.begin() + b, ids.begin() + e, [&](int id) { return bof(id) < bk; }) - ids.begin());
+    }
+    if (mid <= b || mid >= e) { mid = b + n / 2; std::nth_element(ids.begin() + b, ids.begin() + mid, ids.begin() + e, [&](int x, int y) { return key(x) < key(y) || (key(x) == key(y) && x < y); }); }
+    return mid;
+  }
+  int build2(int b, int e, int sp) {  // returns binary node index
+    int ni = (int)bin.size(); bin.emplace_back();
+    int r[2][2] = {{b, sp}, {sp, e}};
+    for (int k = 0; k < 2; k++) {
+      GBox bx; for (int i = r[k][0]; i < r[k][1]; i++) bx.grow(tb[ids[i]]);
+      bin[ni].box[k] = bx;
+      int s2 = split(r[k][0], r[k][1]);
+      if (s2 < 0) { bin[ni].child[k] = (int)lprim.size(); bin[ni].count[k] = r[k][1] - r[k][0]; for (int i = r[k][0]; i < r[k][1]; i++) lprim.push_back(ids[i]); }
+      else { int c = build2(r[k][0], r[k][1], s2); bin[ni].child[k] = c; bin[ni].count[k] = 0; }
+    }
+    return ni;
+  }
+  struct E { GBox box; int child, count; };
+  void collapse(std::vector<E> ents, int gi) {
+    while ((int)ents.size() < width) {
+      int best = -1; float ba = -1;
+      for (size_t i = 0; i < ents.size(); i++) if (ents[i].count == 0 && ents[i].box.area() > ba) { ba = ents[i].box.area(); best = (int)i; }
+      if (best < 0) break;
+      int n2 = ents[best].child; ents.erase(ents.begin() + best);
+      for (int k = 0; k < 2; k++) ents.push_back(E{bin[n2].box[k], bin[n2].child[k], bin[n2].count[k]});
+    }
+    int inner = 0; for (auto& e : ents) inner += e.count == 0;
+    int base = (int)out.nodes.size(); out.nodes.resize(out.nodes.size() + inner);
+    GNode nd; int r = 0;
+    for (auto& e : ents) { nd.box.push_back(e.box); nd.count.push_back(e.count); nd.child.push_back(e.count == 0 ? base + r++ : e.child); }
+    out.nodes[gi] = nd;
+    r = 0;
+    for (auto& e : ents) if (e.count == 0) {
+      int n2 = e.child;
+      collapse({E{bin[n2].box[0], bin[n2].child[0], bin[n2].count[0]}, E{bin[n2].box[1], bin[n2].child[1], bin[n2].count[1]}}, base + r++);
+    }
+  }
+  GTree run() {
+    int n = s.num_tris(); tb.resize(n); cen.resize(n); ids.resize(n);
+    for (int i = 0; i < n; i++) { GBox b; b.grow(s.pos[3 * i]); b.grow(s.pos[3 * i + 1]); b.grow(s.pos[3 * i + 2]); tb[i] = b; cen[i] = (b.lo + b.hi) * 0.5f; ids[i] = i; }
+    int r = build2(0, n, split(0, n));
+    out.nodes.resize(1);
+    collapse({E{bin[r].box[0], bin[r].child[0], bin[r].count[0]}, E{bin[r].box[1], bin[r].child[1], bin[r].count[1]}}, 0);
+    for (auto& nd : out.nodes)  // leaf children of a node: one contiguous range
+      for (size_t k = 0; k < nd.child.size(); k++)
+        if (nd.count[k] > 0) { int f = (int)out.prim.size(); for (int j = 0; j < nd.count[k]; j++) out.prim.push_back(lprim[nd.child[k] + j]); nd.child[k] = f; }
+    return out;
+  }
+};
+
+// Traversal over a generic tree with the engine's step semantics (a step = one node visit and / or
+// one triangle pair).
+int gquery(const GTree& t, const HostScene& s, f3 o, f3 d, float tmin, float tmax, bool any, Stats& st) {
+  f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  float best = tmax;
+  int node = 0, steps = 0, tlo = 0, thi = 0, sp = 0;
+  int stack[256];
+  auto tri = [&](int j, float& tt) {
+    int p = t.prim[j];
+    f3 p0 = s.pos[3 * p], p1 = s.pos[3 * p + 1], p2 = s.pos[3 * p + 2];
+    f3 e0 = p1 - p0, e1 = p0 - p2, n = cross(e1, e0);
+    f3 e2 = (1.0f / dot(n, d)) * (p0 - o);
+    f3 i = cross(d, e2);
+    float beta = dot(i, e1), gamma = dot(i, e0);
+    tt = dot(n, e2);
+    return (tt < (any ? tmax : best)) & (tt > tmin) & (beta >= 0.0f) & (gamma >= 0.0f) & (beta + gamma <= 1.0f);
+  };
+  while (true) {
+    steps++;
+    if (tlo >= thi) {
+      const GNode& nd = t.nodes[node];
+      st.visits++;
+      int lo = 0x7FFFFFFF, hi = 0, m = 0;
+      int c[16]; float kk[16];
+      for (size_t k = 0; k < nd.box.size(); k++) {
+        const GBox& b = nd.box[k];
+        float x0 = (b.lo.x - o.x) * inv.x, x1 = (b.hi.x - o.x) * inv.x, y0 = (b.lo.y - o.y) * inv.y, y1 = (b.hi.y - o.y) * inv.y;
+        float z0 = (b.lo.z - o.z) * inv.z, z1 = (b.hi.z - o.z) * inv.z;
+        float nn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tmin));
+        float ff = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), best));
+        if (!(nn <= ff * 1.00001f + 1e-6f)) continue;
+        if (nd.count[k] > 0) { lo = std::min(lo, nd.child[k]); hi = std::max(hi, nd.child[k] + nd.count[k]); }
+        else { c[m] = nd.child[k]; kk[m] = nn; m++; }
+      }
+      tlo = lo; thi = hi;
+      for (int a = 0; a < m; a++) for (int q = a + 1; q < m; q++) if (kk[q] < kk[a]) { std::swap(kk[q], kk[a]); std::swap(c[q], c[a]); }
+      if (m) { for (int a = m - 1; a >= 1; a--) stack[sp++] = c[a]; node = c[0]; }
+      else if (sp == 0) node = -1;
+      else node = stack[--sp];
+    }
+    if (tlo < thi) {
+      for (int u = 0; u < 2 && tlo < thi; u++) {
+        float tt; st.tris++;
+        if (tri(tlo++, tt)) {
+          if (!any) best = std::min(best, tt);
+          else if (s.mats[s.flags[t.prim[tlo - 1]] & 0xff].type != MATL_REFRACTION) return steps;
+        }
+      }
+    }
+    if (tlo >= thi && node < 0) return steps;
+  }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -143,6 +289,24 @@ int main(int argc, char** argv) {
   const auto t0 = std::chrono::steady_clock::now();
   build_bvh(s, b);
   const double build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (const char* wv = getenv("FOVRT_STUDY_WIDTH")) {  // generic-width study tree instead of the engine's
+    GBuilder gb{s, atoi(wv)};
+    GTree t = gb.run();
+    Stats g[2];
+    double tot = 0;
+    const size_t nq = q.size() / 2;
+    for (size_t i = 0; i < nq; i++) {
+      const f4 a = q[2 * i], d = q[2 * i + 1];
+      const bool any = d.w != 0.0f;
+      const int st = gquery(t, s, mk3(a.x, a.y, a.z), mk3(d.x, d.y, d.z), 1e-3f, a.w, any, g[any]);
+      g[any].steps += st; g[any].n++; tot += st;
+    }
+    printf("width %d: nodes %zu\n", gb.width, t.nodes.size());
+    for (int k = 0; k < 2; k++)
+      printf("  %-7s steps %6.2f visits %6.2f tris %6.2f\n", k ? "shadow" : "closest", g[k].steps / g[k].n, g[k].visits / g[k].n, g[k].tris / g[k].n);
+    printf("  all     steps %6.2f visits %6.2f tris %6.2f\n", tot / nq, (g[0].visits + g[1].visits) / nq, (g[0].tris + g[1].tris) / nq);
+    return 0;
+  }
   const char* mv = getenv("FOVRT_STUDY_MASK");
   Sim sim{b, s, mv && atoi(mv) != 0};
   Stats st[2];  // closest, shadow

@@ -311,6 +311,34 @@ def test_frame_driver_equals_stage_calls(fovrt_mod, timing):
         assert equal_nan(a.read(tid), b.read(tid)), tid
 
 
+@pytest.mark.parametrize("slots", ["3", "2"])
+def test_pipelined_frames_panning_equal_stage_calls(fovrt_mod, monkeypatch, slots):
+    """fr_frame pipelining (front stages of frame N+1 beside entry 3 of frame N, reconstruction inputs and
+    the trace tail's WEIGHT / mask / active list rotating over FOVRT_SLOTS frame slots) against the
+    synchronous stage calls: 8 frames (the slots wrap around more than twice), the camera panning every
+    frame, so every frame's shading reprojects the previous history; all outputs bit-identical."""
+    monkeypatch.setenv("FOVRT_SLOTS", slots)
+    W, H = 320, 192
+    a = make_tracer(fovrt_mod, W, H, scene=1, mask=1, spp=4, dmd=3)
+    b = make_tracer(fovrt_mod, W, H, scene=1, mask=1, spp=4, dmd=3)
+    cam = fovrt_mod.Camera.preset(1, W, H)
+    for f in range(8):
+        cam.setPrevState()
+        cam.lookAt(np.asarray(cam.target) + np.array([0.01, 0.005, 0.0], np.float32))
+        a.update_optix_variables(cam)
+        b.update_optix_variables(cam)
+        a.frame(timing=False)
+        b.geometry_launch(); b.sampling_launch(); b.optimize_launch(); b.shading_launch()
+        fovrt_mod.JumpFlooding(b).render(TN.SHADING)
+        fovrt_mod.SibsonInterpolation(b).render()
+        fovrt_mod.PullPushInterpolation(b).render(TN.SHADING)
+        fovrt_mod.ATrous(b).render(1, TN.POSITION, TN.NORMAL, TN.PULLPUSH)
+    for tid in (TN.SHADING, TN.JFA_COLOR, TN.SIBSON, TN.PULLPUSH, TN.ATROUS, TN.HISTORY_CACHE, TN.POSITION,
+                TN.NORMAL, TN.DEPTH_CACHE, TN.WEIGHT, TN.MASK):
+        assert equal_nan(a.read(tid), b.read(tid)), tid
+    assert a.ray_count() == b.ray_count()
+
+
 def test_kernel_timing_counts_frames_and_leaves_results_unchanged(fovrt_mod):
     """fr_kernel_timing: live HIP events around entry 3 of pipelined frames (what bench.py reports)."""
     W, H, K = 128, 128, 40  # more frames than the 32-slot event ring: slots are harvested on reuse
