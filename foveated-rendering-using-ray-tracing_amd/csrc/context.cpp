@@ -48,6 +48,7 @@ bool gpu_build_bvh(const f3*, int, BvhNode**, TriGeo**, int32_t**, int*, int*, h
 void launch_trace_queries(const DevScene&, const f4*, uint32_t, f4*, uint32_t*, hipStream_t, int);
 void diag_record_queries(f4*, uint32_t, hipStream_t);
 uint32_t diag_recorded_queries(hipStream_t);
+void diag_sample_trace(uint32_t*, uint32_t, uint32_t*, uint32_t, hipStream_t);
 #endif
 void launch_pullpush(const f4*, f4*, f4*, f4*, f4*, int, int, hipStream_t);
 void launch_atrous(const f4*, const f4*, const f4*, f4*, int, int, float, float, float, float, hipStream_t);
@@ -1173,6 +1174,31 @@ int fr_set_positions(fr_ctx* c, const float* xyz, size_t ntris) {
 }
 
 #ifdef FR_STAMPS
+// Diagnostic probe (libfovrt_diag.so only, not part of the ABI): one shading launch (geometry /
+// sampling / optimize must have run) with per-sample records (queries, traversal steps, start, end;
+// s_memrealtime ticks) and per-wave records (start, refill dry, end, samples), copied to the host.
+extern "C" int fr_diag_sample_trace(fr_ctx* c, uint32_t* srec, uint32_t scap, uint32_t* wrec, uint32_t wcap) {
+  if (!c || !srec || !wrec) return FR_E_INVALID;
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  uint32_t *ds = nullptr, *dw = nullptr;
+  HIP_TRY(c, hipMalloc(&ds, (size_t)scap * 16));
+  HIP_TRY(c, hipMalloc(&dw, (size_t)wcap * 16));
+  hipMemsetAsync(ds, 0, (size_t)scap * 16, c->stream);
+  hipMemsetAsync(dw, 0, (size_t)wcap * 16, c->stream);
+  diag_sample_trace(ds, scap, dw, wcap, c->stream);
+  int rc = enqueue_shading(c);
+  diag_sample_trace(nullptr, 0, nullptr, 0, c->stream);
+  hipStreamSynchronize(c->stream);
+  if (!rc) {
+    HIP_TRY(c, hipMemcpy(srec, ds, (size_t)scap * 16, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(wrec, dw, (size_t)wcap * 16, hipMemcpyDeviceToHost));
+  }
+  hipFree(ds);
+  hipFree(dw);
+  return rc;
+}
+
 // Diagnostic probe (libfovrt_diag.so only, not part of the ABI): records every query of one shading
 // launch (geometry / sampling / optimize must have run), then traces the recorded stream with
 // k_trace_queries. out = {queries, best ms of 5 runs, shadow queries, ms of the stream partitioned by
