@@ -311,6 +311,32 @@ def test_frame_driver_equals_stage_calls(fovrt_mod, timing):
         assert equal_nan(a.read(tid), b.read(tid)), tid
 
 
+@pytest.mark.parametrize("chunk", ["64", "4"])
+def test_megakernel_schedule_does_not_change_samples(fovrt_mod, monkeypatch, chunk):
+    """The megakernel's work queue (k_shade_paths): at 1080p the launch has between 1 and 8 samples per
+    lane, so the refraction class is handed out in small chunks spread over all waves (the adaptive
+    policy). Fixed 64-slot and 4-slot chunks (FOVRT_SHADE_CHUNK_REFR, read at fr_create) schedule the
+    same samples differently: every slot must still be traced exactly once, and a sample's value does
+    not depend on the lane or the time it runs, so SHADING and the history are bit-identical."""
+    W, H = 1920, 1080
+    monkeypatch.delenv("FOVRT_SHADE_CHUNK_REFR", raising=False)
+    a = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=1)
+    monkeypatch.setenv("FOVRT_SHADE_CHUNK_REFR", chunk)
+    b = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=1)
+    for t in (a, b):
+        t.update_optix_variables(fovrt_mod.Camera.preset(1, W, H))
+    for _ in range(2):
+        for t in (a, b):
+            t.geometry_launch(); t.sampling_launch(); t.optimize_launch(); t.shading_launch()
+    assert a.ray_count() == b.ray_count() and a.ray_count() * 4 > 1536 * 128  # >= 1 sample per lane
+    for tid in (TN.SHADING, TN.HISTORY_CACHE):
+        assert equal_nan(a.read(tid), b.read(tid)), tid
+    st_a, st_b = a.stats(), b.stats()
+    for k in ("primary", "shadow", "mirror", "refraction", "reflection"):
+        assert st_a[k] == st_b[k], k
+    a.destroy(); b.destroy()
+
+
 @pytest.mark.parametrize("slots", ["3", "2"])
 def test_pipelined_frames_panning_equal_stage_calls(fovrt_mod, monkeypatch, slots):
     """fr_frame pipelining (front stages of frame N+1 beside entry 3 of frame N, reconstruction inputs and
