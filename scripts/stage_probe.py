@@ -10,10 +10,14 @@ import fovrt
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 W, H = 3840, 2160
-t = fovrt.PathTracer(fovrt.Config(width=W, height=H, scene=fovrt.SCENE_BUNNY, mask_mode=fovrt.MASK_LOGPOLAR_SIGNED,
-                                  spp=4, diffuse_max_depth=3))
+# FOVRT_PROBE_SCENE=vokselia: configs[4]'s view (8 spp, saliency mask); default: the bench workload
+VOK = os.environ.get("FOVRT_PROBE_SCENE") == "vokselia"
+scene = fovrt.SCENE_VOKSELIA if VOK else fovrt.SCENE_BUNNY
+t = fovrt.PathTracer(fovrt.Config(width=W, height=H, scene=scene,
+                                  mask_mode=fovrt.MASK_SALIENCY if VOK else fovrt.MASK_LOGPOLAR_SIGNED,
+                                  spp=8 if VOK else 4, diffuse_max_depth=3))
 t.initialize()
-t.update_optix_variables(fovrt.Camera.preset(fovrt.SCENE_BUNNY, W, H))
+t.update_optix_variables(fovrt.Camera.preset(scene, W, H))
 for _ in range(3):
     t.frame(False)
 t.synchronize()
