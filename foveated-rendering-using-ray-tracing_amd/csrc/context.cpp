@@ -21,7 +21,7 @@
 namespace fr {
 void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
 void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
-                        const f4*, uint32_t*, f4*, DevStats*, f4*, uint32_t*, uint32_t, hipStream_t);
+                        const f4*, uint32_t*, f4*, DevStats*, f4*, uint32_t*, uint32_t, uint32_t, hipStream_t);
 void launch_sample_setup(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*, f4*,
                          uint32_t*, hipStream_t);
 void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
@@ -132,6 +132,7 @@ struct fr_ctx {
   uint32_t* aux_seed = nullptr;   // per active pixel: the seed after the two draws
   u2 *jfa_a = nullptr, *jfa_b = nullptr;  // JFA state ping-pong (seed coord texel + alpha flags)
   uint32_t chunk_refr = 0;  // fixed refraction-class chunk of the megakernel (FOVRT_SHADE_CHUNK_REFR), 0 adaptive
+  uint32_t xcd_bands = 1;   // megakernel queue: per-XCD class bands (FOVRT_SHADE_XCD_BANDS=0: interleaved chunks)
   float* ftab = nullptr;  // texel-centre coordinates ((x + 0.5) / W, x < W; then (y + 0.5) / H)
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
   f4 *sib_prefix = nullptr, *sib_blocks = nullptr;  // Sibson run form: per-row block prefix sums + block totals
@@ -482,6 +483,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   for (auto& e : c->ev_trace) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->ev_recon) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (const char* v = getenv("FOVRT_SHADE_CHUNK_REFR")) c->chunk_refr = (uint32_t)std::max(0, atoi(v));
+  if (const char* v = getenv("FOVRT_SHADE_XCD_BANDS")) c->xcd_bands = atoi(v) != 0;
   {  // FOVRT_SLOTS: frame slots of the pipelined loop (2 or 3; A/B knob)
     const char* v = getenv("FOVRT_SLOTS");
     if (v) c->nslots = std::max(2, std::min(fr_ctx::MAX_SLOTS, atoi(v)));
@@ -775,7 +777,7 @@ static int enqueue_shading(fr_ctx* c) {
   if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
   if (kt) hipEventRecord(kt[1], c->stream);
   launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache],
-                     c->shade_ctr, c->samples, c->stats, c->aux, c->aux_seed, c->chunk_refr, c->stream);
+                     c->shade_ctr, c->samples, c->stats, c->aux, c->aux_seed, c->chunk_refr, c->xcd_bands, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   if (kt) hipEventRecord(kt[2], c->stream);
   hipStreamWaitEvent(c->stream, c->ev[12], 0);

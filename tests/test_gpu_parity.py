@@ -311,17 +311,21 @@ def test_frame_driver_equals_stage_calls(fovrt_mod, timing):
         assert equal_nan(a.read(tid), b.read(tid)), tid
 
 
-@pytest.mark.parametrize("chunk", ["64", "4"])
-def test_megakernel_schedule_does_not_change_samples(fovrt_mod, monkeypatch, chunk):
+@pytest.mark.parametrize("chunk,bands", [("64", "1"), ("4", "1"), ("0", "0"), ("64", "0")])
+def test_megakernel_schedule_does_not_change_samples(fovrt_mod, monkeypatch, chunk, bands):
     """The megakernel's work queue (k_shade_paths): at 1080p the launch has between 1 and 8 samples per
     lane, so the refraction class is handed out in small chunks spread over all waves (the adaptive
-    policy). Fixed 64-slot and 4-slot chunks (FOVRT_SHADE_CHUNK_REFR, read at fr_create) schedule the
-    same samples differently: every slot must still be traced exactly once, and a sample's value does
-    not depend on the lane or the time it runs, so SHADING and the history are bit-identical."""
+    policy), and each XCD takes one band of every primary-hit class. Fixed 64-slot and 4-slot chunks
+    (FOVRT_SHADE_CHUNK_REFR) and chunks interleaved over the XCDs (FOVRT_SHADE_XCD_BANDS=0), both read at
+    fr_create, schedule the same samples differently: every slot must still be traced exactly once,
+    and a sample's value does not depend on the lane or the time it runs, so SHADING and the history
+    are bit-identical."""
     W, H = 1920, 1080
     monkeypatch.delenv("FOVRT_SHADE_CHUNK_REFR", raising=False)
+    monkeypatch.delenv("FOVRT_SHADE_XCD_BANDS", raising=False)
     a = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=1)
     monkeypatch.setenv("FOVRT_SHADE_CHUNK_REFR", chunk)
+    monkeypatch.setenv("FOVRT_SHADE_XCD_BANDS", bands)
     b = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=1)
     for t in (a, b):
         t.update_optix_variables(fovrt_mod.Camera.preset(1, W, H))
