@@ -202,6 +202,9 @@ def main():
                     help="views rendered by the job (0: one per rank = weak scaling); the ranks of a view "
                          "tile-shard it and gather the tiles to the view's first rank for reconstruction")
     ap.add_argument("--tile", type=int, default=128, help="screen tile size of the tile sharding")
+    ap.add_argument("--root-traces", action="store_true",
+                    help="tile sharding: the view's compositing rank also traces tiles (default: its tiles go to "
+                         "the other ranks, and it runs the G-buffer and the reconstruction half only)")
     ap.add_argument("--composite", action="store_true",
                     help="every frame, gather the views' reconstructed images to rank 0 over RCCL and compose them "
                          "side by side (the final composite of the stereo configuration)")
@@ -261,7 +264,10 @@ def main():
 
     slab = gather_list = None
     if G > 1:
-        tracer.set_shard(vrank, G, args.tile)
+        # the compositing rank runs the reconstruction half, which no other rank can share (JFA's
+        # reach, the global pull-push pyramid): by default it traces no tiles (fr_set_shard_ex)
+        first_tracer = 0 if args.root_traces else 1
+        tracer.set_shard(vrank, G, args.tile, first_tracer)
         n_tex = tracer.shard_texels()
         slab = torch.empty(n_tex * 4, dtype=torch.float32, device=f"cuda:{device}")
         if vrank == 0:
@@ -384,7 +390,10 @@ def main():
 
     K = args.steps
     avg = {k[:-3]: v / n_timed for k, v in stage_ms.items()}
-    rho = float(np.mean(ray_counts)) * G / (W * H)
+    # foveal density: the active pixels of all ranks of all views (a tile-sharded view's ranks each trace
+    # a part; with first_tracer 1 the compositing rank traces none)
+    _, count_sum = reduce_over_ranks(dist, dev, 0.0, float(np.mean(ray_counts)))
+    rho = count_sum / views / (W * H)
     L = jfa_passes(W, H)
     sb = stage_bytes(W, H, rho, args.spp, L)
     # (a non-compositing rank of a tile-sharded view runs no reconstruction: its image stages are 0 ms)
@@ -428,7 +437,8 @@ def main():
                    "composite": bool(args.composite and views > 1), "camera_step": args.pan,
                    "parallelism": (f"views x{world} (one view per GPU)" if G == 1 else
                                    f"{views} view(s) x {G}-way {args.tile}px tile sharding, RCCL gather to the "
-                                   f"view's first rank"),
+                                   f"view's first rank" + ("" if args.root_traces else
+                                                          ", which traces no tiles and reconstructs")),
                    "procedural_meshes": "box/bunny/earth stand-ins (the reference's .obj files are absent)"},
         "fps": round(K / elapsed, 2),
         "frames_per_s_total": round(views * K / elapsed, 2),

@@ -594,7 +594,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   U.spp = cfg.spp;
   U.sqrt_spp = (int)floor(sqrt((double)cfg.spp) + 1e-9);
   U.mask_mode = cfg.mask_mode;
-  U.shard_rank = 0; U.shard_count = 1; U.shard_tile = 128; U.shard_tiles_x = (c->W + 127) / 128;
+  U.shard_rank = 0; U.shard_count = 1; U.shard_tile = 128; U.shard_tiles_x = (c->W + 127) / 128; U.shard_first = 0;
   {
     fr_camera_pose pose;
     float eye[3], tgt[3], upv[3] = {0, 1, 0};
@@ -1017,24 +1017,29 @@ int fr_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, true, true
 int fr_trace_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, true, false); }
 int fr_reconstruct_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, false, true); }
 
-int fr_set_shard(fr_ctx* c, int rank, int count, int tile) {
+int fr_set_shard_ex(fr_ctx* c, int rank, int count, int tile, int first_tracer) {
   if (!c) return FR_E_INVALID;
   if (count < 1 || rank < 0 || rank >= count || tile < 8 || tile > 4096)
     return fail(c, FR_E_INVALID, "fr_set_shard: need 0 <= rank < count and 8 <= tile <= 4096");
+  if (first_tracer < 0 || (count > 1 && first_tracer >= count) || (count == 1 && first_tracer != 0))
+    return fail(c, FR_E_INVALID, "fr_set_shard_ex: need 0 <= first_tracer < count (at least one tracing rank)");
   c->U.shard_rank = rank;
   c->U.shard_count = count;
   c->U.shard_tile = tile;
   c->U.shard_tiles_x = (c->W + tile - 1) / tile;
+  c->U.shard_first = first_tracer;
   c->compacted = false;
   return FR_OK;
 }
+int fr_set_shard(fr_ctx* c, int rank, int count, int tile) { return fr_set_shard_ex(c, rank, count, tile, 0); }
 
 int fr_shard_texels(fr_ctx* c, size_t* texels) {
   if (!c || !texels) return FR_E_INVALID;
   const int T = c->U.shard_count > 1 ? c->U.shard_tile : 0;
   if (!T) { *texels = (size_t)c->W * c->H; return FR_OK; }
   const size_t tiles = (size_t)c->U.shard_tiles_x * ((c->H + T - 1) / T);
-  *texels = (tiles + c->U.shard_count - 1) / c->U.shard_count * (size_t)T * T;
+  const size_t tracers = (size_t)(c->U.shard_count - c->U.shard_first);
+  *texels = (tiles + tracers - 1) / tracers * (size_t)T * T;
   return FR_OK;
 }
 

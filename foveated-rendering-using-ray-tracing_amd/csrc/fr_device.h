@@ -99,9 +99,10 @@ struct FrameUniforms {
   int32_t spp;
   int32_t sqrt_spp;
   int32_t mask_mode;
-  // screen-tile sharding of one view across ranks (fr_set_shard): tile t = ty * tiles_x + tx is
-  // traced by rank t % shard_count; shard_count 1 = the whole screen
-  int32_t shard_rank, shard_count, shard_tile, shard_tiles_x;
+  // screen-tile sharding of one view across ranks (fr_set_shard_ex): tile t = ty * tiles_x + tx is
+  // traced by rank shard_first + t % (shard_count - shard_first); ranks below shard_first (the view's
+  // reconstruction root) trace none; shard_count 1 = the whole screen
+  int32_t shard_rank, shard_count, shard_tile, shard_tiles_x, shard_first;
 };
 
 // XCD-aware block order: blocks b, b+8, b+16, ... share an XCD (and its L2), so hand each of the 8
@@ -113,10 +114,13 @@ FR_DEV uint32_t xcd_tile(uint32_t bx, uint32_t by, uint32_t gx, uint32_t gy) {
   return k * q + (k < r ? k : r) + i;
 }
 
+FR_HD int shard_owner(const FrameUniforms& U, int t) {
+  return U.shard_first + t % (U.shard_count - U.shard_first);
+}
 FR_HD bool shard_owns(const FrameUniforms& U, int x, int y) {
   if (U.shard_count <= 1) return true;
   const int t = (y / U.shard_tile) * U.shard_tiles_x + x / U.shard_tile;
-  return t % U.shard_count == U.shard_rank;
+  return shard_owner(U, t) == U.shard_rank;
 }
 
 // Ray-segment statistics, accumulated with one atomic per wave.

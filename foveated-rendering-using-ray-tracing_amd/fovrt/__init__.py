@@ -131,6 +131,7 @@ _SIGS = {
     "fr_trace_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_reconstruct_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_set_shard": [C.c_void_p, C.c_int, C.c_int, C.c_int],
+    "fr_set_shard_ex": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int],
     "fr_shard_texels": [C.c_void_p, C.POINTER(C.c_size_t)],
     "fr_shard_pack": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_shard_unpack": [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t],
@@ -477,8 +478,9 @@ class PathTracer:
         self._check(_lib.fr_set_gaze(self._ctx, float(x), float(y)))
 
     # tile sharding of one view across ranks (include/fovrt.h, fr_set_shard)
-    def set_shard(self, rank, count, tile=128):
-        self._check(_lib.fr_set_shard(self._ctx, int(rank), int(count), int(tile)))
+    def set_shard(self, rank, count, tile=128, first_tracer=0):
+        """fr_set_shard_ex: tiles dealt round robin over ranks first_tracer .. count-1."""
+        self._check(_lib.fr_set_shard_ex(self._ctx, int(rank), int(count), int(tile), int(first_tracer)))
 
     def shard_texels(self) -> int:
         n = C.c_size_t()

@@ -228,6 +228,11 @@ int fr_synchronize(fr_ctx* ctx);
  * whole screen. Slabs are device buffers of fr_shard_texels() RGBA32F texels (T*T per owned tile,
  * owned tiles in increasing order); pack/unpack synchronise the context stream. */
 int fr_set_shard(fr_ctx* ctx, int rank, int count, int tile);
+/* The same with the tiles dealt over ranks first_tracer .. count-1 only (tile t to rank
+ * first_tracer + t % (count - first_tracer)); ranks below first_tracer trace nothing. first_tracer = 1
+ * leaves the view's compositing rank 0 to the G-buffer and the reconstruction half, which no other
+ * rank can share (JFA's reach, the global pull-push pyramid). fr_set_shard = first_tracer 0. */
+int fr_set_shard_ex(fr_ctx* ctx, int rank, int count, int tile, int first_tracer);
 int fr_shard_texels(fr_ctx* ctx, size_t* texels);
 int fr_shard_pack(fr_ctx* ctx, int buffer_id, void* device_slab, size_t bytes);
 int fr_shard_unpack(fr_ctx* ctx, int buffer_id, int src_rank, const void* device_slab, size_t bytes);

@@ -449,14 +449,15 @@ def test_cpp_facade_driver_matches_python(fovrt_mod, tmp_path):
 # unpacks the others' shading tiles and reconstructs; the composite equals the one-GPU frame.
 # Rehearsed here with three contexts on one device (one process), slabs in torch device memory.
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("nranks,tile", [(2, 64), (3, 32)])
-def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile):
+@pytest.mark.parametrize("nranks,tile,first", [(2, 64, 0), (3, 32, 0), (2, 64, 1), (3, 32, 1), (4, 16, 1)])
+def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile, first):
+    """first = 1 (fr_set_shard_ex, the bench default): the compositing rank traces no tiles."""
     import torch
     W, H = 200, 136  # not multiples of the tile: clipped border tiles
     full = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
     ranks = [make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3) for _ in range(nranks)]
     for r, t in enumerate(ranks):
-        t.set_shard(r, nranks, tile)
+        t.set_shard(r, nranks, tile, first)
     n = ranks[0].shard_texels()
     assert all(t.shard_texels() == n for t in ranks)
     slabs = [torch.zeros(n * 4, dtype=torch.float32, device="cuda") for _ in range(nranks)]
@@ -470,6 +471,7 @@ def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile):
             root.shard_unpack(TN.SHADING, r, slabs[r].data_ptr(), n * 16)
         root.reconstruct_frame(timing=False)
         assert sum(counts) == full.ray_count()
+        assert first == 0 or counts[0] == 0
         assert equal_nan(root.read(TN.SHADING), full.read(TN.SHADING))
     for tid in (TN.JFA_COLOR, TN.SIBSON, TN.PULLPUSH, TN.ATROUS):
         assert equal_nan(root.read(tid), full.read(tid)), tid
