@@ -202,6 +202,9 @@ def main():
                     help="views rendered by the job (0: one per rank = weak scaling); the ranks of a view "
                          "tile-shard it and gather the tiles to the view's first rank for reconstruction")
     ap.add_argument("--tile", type=int, default=128, help="screen tile size of the tile sharding")
+    ap.add_argument("--dense-gather", action="store_true",
+                    help="tile sharding with a static camera: gather the ranks' whole tile slabs of SHADING instead "
+                         "of only the pixels they traced (the moving camera always uses the tile slabs)")
     ap.add_argument("--root-traces", action="store_true",
                     help="tile sharding: the view's compositing rank also traces tiles (default: its tiles go to "
                          "the other ranks, and it runs the G-buffer and the reconstruction half only)")
@@ -277,6 +280,14 @@ def main():
         if args.pan:
             hist_slab = torch.empty_like(slab)
             hist_list = [torch.empty_like(slab) for _ in range(G)]
+        # sparse gather (static camera): the traced pixels only, 20 B each (fr_shard_pack_active); a rank
+        # traces at most its tiles' pixels, so n_tex entries always fit
+        sparse = not args.pan and not args.dense_gather
+        if sparse:
+            act = torch.empty(n_tex * 5, dtype=torch.float32, device=f"cuda:{device}")
+            act_list = [torch.empty_like(act) for _ in range(G)] if vrank == 0 else None
+            cnt_t = torch.zeros(1, dtype=torch.int64, device=f"cuda:{device}")
+            cnt_list = [torch.zeros_like(cnt_t) for _ in range(G)]
 
     comp_img = comp_list = comp_out = None
     if roots_group is not None and vrank == 0:
@@ -332,12 +343,27 @@ def main():
         if args.pan:
             exchange_history()
         sync()  # the previous frame's gather of `slab` has finished on torch's stream
-        tracer.shard_pack(fovrt.TextureName.SHADING, slab.data_ptr(), nbytes)
-        gather_slabs(dist, groups[view], slab, gather_list, root)
+        if sparse:
+            cnt_t.fill_(tracer.ray_count())
+            allgather_slabs(dist, groups[view], cnt_t, cnt_list)
+            counts = [int(c.item()) for c in cnt_list]
+            cap = max(max(counts), 1)
+            n_packed = tracer.shard_pack_active(act.data_ptr(), cap)
+            assert n_packed == counts[vrank]
+            gather_slabs(dist, groups[view], act[:cap * 5],
+                         [a[:cap * 5] for a in act_list] if act_list is not None else None, root)
+            if vrank == 0:
+                sync()
+                for r in range(1, G):
+                    tracer.shard_unpack_active(act_list[r].data_ptr(), cap, counts[r])
+        else:
+            tracer.shard_pack(fovrt.TextureName.SHADING, slab.data_ptr(), nbytes)
+            gather_slabs(dist, groups[view], slab, gather_list, root)
         if vrank == 0:
             sync()
-            for r in range(1, G):
-                tracer.shard_unpack(fovrt.TextureName.SHADING, r, gather_list[r].data_ptr(), nbytes)
+            if not sparse:
+                for r in range(1, G):
+                    tracer.shard_unpack(fovrt.TextureName.SHADING, r, gather_list[r].data_ptr(), nbytes)
             rec = tracer.reconstruct_frame(timing=timing)
             if timing:
                 for k in ("jfa_ms", "sibson_ms", "pullpush_ms", "atrous_ms"):
@@ -438,7 +464,9 @@ def main():
                    "parallelism": (f"views x{world} (one view per GPU)" if G == 1 else
                                    f"{views} view(s) x {G}-way {args.tile}px tile sharding, RCCL gather to the "
                                    f"view's first rank" + ("" if args.root_traces else
-                                                          ", which traces no tiles and reconstructs")),
+                                                          ", which traces no tiles and reconstructs") +
+                                   (" (tile slabs of SHADING)" if args.pan or args.dense_gather else
+                                    " (only the traced pixels, 20 B each)")),
                    "procedural_meshes": "box/bunny/earth stand-ins (the reference's .obj files are absent)"},
         "fps": round(K / elapsed, 2),
         "frames_per_s_total": round(views * K / elapsed, 2),

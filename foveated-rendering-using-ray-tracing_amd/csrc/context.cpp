@@ -39,6 +39,8 @@ void launch_shard_pack(const FrameUniforms&, const f4*, f4*, hipStream_t);
 void launch_logpolar(const f4*, f4*, f4*, int, int, f2, hipStream_t);
 void launch_composite(const f4*, int, int, int, f4*, hipStream_t);
 void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
+void launch_shard_pack_active(const uint32_t*, const uint32_t*, uint32_t, const f4*, f4*, uint32_t*, hipStream_t);
+void launch_shard_unpack_active(const f4*, const uint32_t*, uint32_t, f4*, f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
 void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, int, int, hipStream_t);
@@ -1066,6 +1068,37 @@ int fr_shard_pack(fr_ctx* c, int id, void* slab, size_t bytes) {
 }
 int fr_shard_unpack(fr_ctx* c, int id, int src_rank, const void* slab, size_t bytes) {
   return shard_io(c, id, src_rank, const_cast<void*>(slab), bytes, false);
+}
+
+int fr_shard_pack_active(fr_ctx* c, void* slab, uint32_t capacity, uint32_t* count) {
+  if (!c || !slab || !count) return FR_E_INVALID;
+  if (c->U.shard_count <= 1) return fail(c, FR_E_STATE, "fr_shard_*: call fr_set_shard with count > 1 first");
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  HIP_TRY(c, hipMemcpyAsync(count, c->ray_count, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (*count > capacity) return fail(c, FR_E_INVALID, "fr_shard_pack_active: capacity below the active pixel count");
+  f4* vals = (f4*)slab;
+  uint32_t* idx = (uint32_t*)((char*)slab + (size_t)capacity * sizeof(f4));
+  launch_shard_pack_active(c->active, c->ray_count, capacity, c->img[c->hist_cache], vals, idx, c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FR_OK;
+}
+
+int fr_shard_unpack_active(fr_ctx* c, const void* slab, uint32_t capacity, uint32_t count) {
+  if (!c || !slab) return FR_E_INVALID;
+  if (count > capacity) return fail(c, FR_E_INVALID, "fr_shard_unpack_active: count above capacity");
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  const f4* vals = (const f4*)slab;
+  const uint32_t* idx = (const uint32_t*)((const char*)slab + (size_t)capacity * sizeof(f4));
+  launch_shard_unpack_active(vals, idx, count, c->img[c->hist_cache], c->img[P_shd(c)], c->stream);
+  int rc = check_launch(c);
+  if (rc) return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FR_OK;
 }
 
 int fr_synchronize(fr_ctx* c) {

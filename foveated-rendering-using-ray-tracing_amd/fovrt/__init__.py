@@ -132,6 +132,8 @@ _SIGS = {
     "fr_reconstruct_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_set_shard": [C.c_void_p, C.c_int, C.c_int, C.c_int],
     "fr_set_shard_ex": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int],
+    "fr_shard_pack_active": [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)],
+    "fr_shard_unpack_active": [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32],
     "fr_shard_texels": [C.c_void_p, C.POINTER(C.c_size_t)],
     "fr_shard_pack": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_shard_unpack": [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t],
@@ -495,6 +497,16 @@ class PathTracer:
         """Writes rank src_rank's tiles from the device slab at device_ptr into the buffer."""
         self._check(_lib.fr_shard_unpack(self._ctx, int(buffer_id), int(src_rank), C.c_void_p(device_ptr),
                                          int(nbytes)))
+
+    def shard_pack_active(self, device_ptr, capacity) -> int:
+        """Packs the pixels this rank's last trace half shaded (capacity x 20 B slab); returns their count."""
+        n = C.c_uint32()
+        self._check(_lib.fr_shard_pack_active(self._ctx, C.c_void_p(device_ptr), int(capacity), C.byref(n)))
+        return n.value
+
+    def shard_unpack_active(self, device_ptr, capacity, count):
+        """Scatters another rank's packed pixels into HISTORY_CACHE and SHADING."""
+        self._check(_lib.fr_shard_unpack_active(self._ctx, C.c_void_p(device_ptr), int(capacity), int(count)))
 
     def synchronize(self):
         self._check(_lib.fr_synchronize(self._ctx))

@@ -233,6 +233,15 @@ int fr_set_shard(fr_ctx* ctx, int rank, int count, int tile);
  * leaves the view's compositing rank 0 to the G-buffer and the reconstruction half, which no other
  * rank can share (JFA's reach, the global pull-push pyramid). fr_set_shard = first_tracer 0. */
 int fr_set_shard_ex(fr_ctx* ctx, int rank, int count, int tile, int first_tracer);
+/* Sparse SHADING gather for a static camera (SURVEY §8(e) "sparse variant"): a tracing rank packs only
+ * the pixels its last trace half shaded, as capacity x 16 B of history texels followed by capacity x 4 B
+ * of pixel indices (slab >= 20 x capacity bytes); *count returns their number (FR_E_INVALID when it
+ * exceeds capacity: size capacity from fr_ray_count). The compositing rank, after its own trace half
+ * (which carries every other pixel's history), scatters each rank's entries into HISTORY_CACHE and
+ * SHADING. ~10x less than the tile slabs at a 10 % mask. With a moving camera use the tile slabs and
+ * the HISTORY_CACHE exchange. Both synchronise the context stream. */
+int fr_shard_pack_active(fr_ctx* ctx, void* device_slab, uint32_t capacity, uint32_t* count);
+int fr_shard_unpack_active(fr_ctx* ctx, const void* device_slab, uint32_t capacity, uint32_t count);
 int fr_shard_texels(fr_ctx* ctx, size_t* texels);
 int fr_shard_pack(fr_ctx* ctx, int buffer_id, void* device_slab, size_t bytes);
 int fr_shard_unpack(fr_ctx* ctx, int buffer_id, int src_rank, const void* device_slab, size_t bytes);

@@ -5,7 +5,8 @@ A G-rank view with fr_set_shard_ex(first_tracer = 1): ranks 1..G-1 trace the scr
 computes the G-buffer and sampling (both needed by the reconstruction) and runs the reconstruction half on
 the gathered SHADING. On one GPU this measures, per G, the work of one tracing rank (its whole trace half,
 timed frames, median) and of the compositing rank (its front stages + the reconstruction half), plus the
-slab each tracer sends. The gather over xGMI is not measured here (one GPU): it is priced at an assumed
+slab each tracer sends: its traced pixels, 20 B each (the sparse gather, bench.py's default for a static
+camera; the tile slabs of SHADING are reported beside it). The gather over xGMI is not measured here (one GPU): it is priced at an assumed
 link rate (each tracer has its own link to the root). Prints one JSON line per G.
   python scripts/shard_model.py [scene=bunny|vokselia] [xgmi_GBs=64]"""
 import json
@@ -50,14 +51,16 @@ def main():
     for G in (2, 4, 8):
         t.set_shard(1, G, 128, 1)  # one tracing rank
         tr = med(lambda: t.trace_frame(timing=True))
-        slab = t.shard_texels() * 16
+        dense = t.shard_texels() * 16
+        slab = t.ray_count() * 20  # the sparse gather (fr_shard_pack_active): the traced pixels only
         t.set_shard(0, G, 128, 1)  # the compositing rank: front stages (G-buffer, sampling), no tiles
         front = med(lambda: t.trace_frame(timing=True))
         gather = slab / (link * 1e9) * 1e3
         # ranks overlap across frames: tracers trace frame N+1 while the root reconstructs frame N
         frame = max(tr + gather, front + gather + recon)
         print(json.dumps({"G": G, "scene": scene_name, "tracer_trace_ms": round(tr, 4), "root_front_ms": round(front, 4),
-                          "root_recon_ms": round(recon, 4), "slab_MB_per_tracer": round(slab / 1e6, 1),
+                          "root_recon_ms": round(recon, 4), "slab_MB_per_tracer": round(slab / 1e6, 2),
+                          "dense_slab_MB_per_tracer": round(dense / 1e6, 1),
                           "gather_ms_at_%gGBs" % link: round(gather, 4), "model_frame_ms": round(frame, 4),
                           "model_fps": round(1e3 / frame, 1)}))
     t.destroy()

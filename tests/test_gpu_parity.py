@@ -449,9 +449,13 @@ def test_cpp_facade_driver_matches_python(fovrt_mod, tmp_path):
 # unpacks the others' shading tiles and reconstructs; the composite equals the one-GPU frame.
 # Rehearsed here with three contexts on one device (one process), slabs in torch device memory.
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("nranks,tile,first", [(2, 64, 0), (3, 32, 0), (2, 64, 1), (3, 32, 1), (4, 16, 1)])
-def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile, first):
-    """first = 1 (fr_set_shard_ex, the bench default): the compositing rank traces no tiles."""
+@pytest.mark.parametrize("nranks,tile,first,sparse", [(2, 64, 0, False), (3, 32, 0, False), (2, 64, 1, False),
+                                                     (3, 32, 1, False), (4, 16, 1, False), (3, 32, 0, True),
+                                                     (2, 64, 1, True), (4, 16, 1, True)])
+def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile, first, sparse):
+    """first = 1 (fr_set_shard_ex, the bench default): the compositing rank traces no tiles. sparse: the
+    gather sends only the traced pixels (fr_shard_pack_active / fr_shard_unpack_active) instead of the
+    ranks' tile slabs of SHADING."""
     import torch
     W, H = 200, 136  # not multiples of the tile: clipped border tiles
     full = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
@@ -465,10 +469,18 @@ def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile, first)
     for _ in range(3):
         full.frame(timing=False)
         counts = [t.trace_frame(timing=True)["ray_count"] for t in ranks]
-        for r, t in enumerate(ranks):
-            t.shard_pack(TN.SHADING, slabs[r].data_ptr(), n * 16)
-        for r in range(1, nranks):
-            root.shard_unpack(TN.SHADING, r, slabs[r].data_ptr(), n * 16)
+        if sparse:
+            cap = max(counts)
+            act = [torch.zeros(cap * 5 + 1, dtype=torch.float32, device="cuda") for _ in range(nranks)]
+            packed = [t.shard_pack_active(act[r].data_ptr(), cap) for r, t in enumerate(ranks)]
+            assert packed == counts
+            for r in range(1, nranks):
+                root.shard_unpack_active(act[r].data_ptr(), cap, packed[r])
+        else:
+            for r, t in enumerate(ranks):
+                t.shard_pack(TN.SHADING, slabs[r].data_ptr(), n * 16)
+            for r in range(1, nranks):
+                root.shard_unpack(TN.SHADING, r, slabs[r].data_ptr(), n * 16)
         root.reconstruct_frame(timing=False)
         assert sum(counts) == full.ray_count()
         assert first == 0 or counts[0] == 0
