@@ -21,11 +21,12 @@
 namespace fr {
 void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
 void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
-                        const f4*, uint32_t*, f4*, DevStats*, f4*, uint32_t*, uint32_t, uint32_t, hipStream_t);
+                        const f4*, uint32_t*, f4*, unsigned long long*, DevStats*, f4*, uint32_t*, uint32_t, uint32_t,
+                        uint32_t, hipStream_t);
 void launch_sample_setup(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*, f4*,
                          uint32_t*, hipStream_t);
 void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
-                          const f4*, f4*, f4*, uint32_t*, hipStream_t);
+                          const f4*, unsigned long long*, f4*, f4*, uint32_t*, uint32_t, hipStream_t);
 size_t shade_counter_words();
 void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
 void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
@@ -129,12 +130,14 @@ struct fr_ctx {
   uint32_t* ray_count = nullptr;  // ray_count_p[slot]
   uint32_t* active = nullptr;     // active_p[slot]
   uint32_t* shade_ctr = nullptr;  // sharded chunk counters of the shading work queue
-  f4* samples = nullptr;          // one radiance value per (active pixel, camera sample)
+  f4* samples = nullptr;          // one radiance value per (active pixel, camera sample): 16 B, or 32 B fixed point
+  unsigned long long* sample_help = nullptr;  // fixed-point shares of the lanes that took over items, 32 B per sample
   f4* aux = nullptr;              // per active pixel: NDC position, r1, r2 (k_sample_setup)
   uint32_t* aux_seed = nullptr;   // per active pixel: the seed after the two draws
   u2 *jfa_a = nullptr, *jfa_b = nullptr;  // JFA state ping-pong (seed coord texel + alpha flags)
   uint32_t chunk_refr = 0;  // fixed refraction-class chunk of the megakernel (FOVRT_SHADE_CHUNK_REFR), 0 adaptive
   uint32_t xcd_bands = 1;   // megakernel queue: per-XCD class bands (FOVRT_SHADE_XCD_BANDS=0: interleaved chunks)
+  uint32_t handoff = 1;     // megakernel tail handoff (FOVRT_SHADE_HANDOFF): 0 never, 1 small launches, 2 always
   float* ftab = nullptr;  // texel-centre coordinates ((x + 0.5) / W, x < W; then (y + 0.5) / H)
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
   f4 *sib_prefix = nullptr, *sib_blocks = nullptr;  // Sibson run form: per-row block prefix sums + block totals
@@ -486,6 +489,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   for (auto& e : c->ev_recon) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (const char* v = getenv("FOVRT_SHADE_CHUNK_REFR")) c->chunk_refr = (uint32_t)std::max(0, atoi(v));
   if (const char* v = getenv("FOVRT_SHADE_XCD_BANDS")) c->xcd_bands = atoi(v) != 0;
+  if (const char* v = getenv("FOVRT_SHADE_HANDOFF")) c->handoff = (uint32_t)std::min(std::max(atoi(v), 0), 2);
   {  // FOVRT_SLOTS: frame slots of the pipelined loop (2 or 3; A/B knob)
     const char* v = getenv("FOVRT_SLOTS");
     if (v) c->nslots = std::max(2, std::min(fr_ctx::MAX_SLOTS, atoi(v)));
@@ -572,7 +576,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       dalloc(&c->tiles, 1024) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
       dalloc(&c->pull, atlas) != hipSuccess || dalloc(&c->push, atlas) != hipSuccess ||
       dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess ||
-      dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, N * cfg.spp) != hipSuccess ||
+      dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, 2 * N * cfg.spp) != hipSuccess ||
+      dalloc(&c->sample_help, 4 * N * cfg.spp) != hipSuccess ||
       dalloc(&c->aux, N) != hipSuccess || dalloc(&c->aux_seed, N) != hipSuccess ||
       (cfg.sibson_mode == 0 && (dalloc(&c->sib_prefix, (size_t)(c->W + 1) * c->H) != hipSuccess ||
                                 dalloc(&c->sib_blocks, (size_t)sibson_prefix_blocks(c->W) * c->H) != hipSuccess))) {
@@ -629,7 +634,7 @@ int fr_destroy(fr_ctx* c) {
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
   for (int k = 0; k < fr_ctx::MAX_SLOTS; k++) { fr(c->mask_p[k]); fr(c->ray_count_p[k]); fr(c->active_p[k]); }
-  fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->aux); fr(c->aux_seed); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
+  fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->ev_front) hipEventDestroy(c->ev_front);
@@ -779,12 +784,13 @@ static int enqueue_shading(fr_ctx* c) {
   if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
   if (kt) hipEventRecord(kt[1], c->stream);
   launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache],
-                     c->shade_ctr, c->samples, c->stats, c->aux, c->aux_seed, c->chunk_refr, c->xcd_bands, c->stream);
+                     c->shade_ctr, c->samples, c->sample_help, c->stats, c->aux, c->aux_seed, c->chunk_refr,
+                     c->xcd_bands, c->handoff, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   if (kt) hipEventRecord(kt[2], c->stream);
   hipStreamWaitEvent(c->stream, c->ev[12], 0);
   launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache], c->samples,
-                       c->img[c->hist_cur], c->img[P_shd(c)], c->shade_ctr, c->stream);
+                       c->sample_help, c->img[c->hist_cur], c->img[P_shd(c)], c->shade_ctr, c->handoff, c->stream);
   if (kt) hipEventRecord(kt[3], c->stream);
   // this slot's WEIGHT / mask / active list are free for the front stages of frame + nslots after this
   hipEventRecord(c->ev_trace[c->slot], c->stream);

@@ -341,6 +341,38 @@ def test_megakernel_schedule_does_not_change_samples(fovrt_mod, monkeypatch, chu
     a.destroy(); b.destroy()
 
 
+@pytest.mark.parametrize("W,H,spp", [(1920, 1080, 4), (256, 256, 8)])
+def test_megakernel_tail_handoff(fovrt_mod, monkeypatch, W, H, spp):
+    """The small-launch form of k_shade_paths (SampleSum): fixed-point sample sums, and idle lanes of a
+    dry wave take pending refraction/reflection items of their busy neighbours. FOVRT_SHADE_HANDOFF=1 (the
+    default) uses it below 8 samples per lane, which covers 1080p and 256x256; 2 forces it, 0 turns it
+    off (fp32 running sums, the oracle's order). The default and the forced form are bit-identical
+    (the same form; which lanes run an item does not change the integer sums); the fp32 form differs only
+    by the rounding of the sums: per channel RMSE <= 1e-6, max 1e-4 on the tone-mapped colour."""
+    monkeypatch.delenv("FOVRT_SHADE_CHUNK_REFR", raising=False)
+    monkeypatch.delenv("FOVRT_SHADE_XCD_BANDS", raising=False)
+    tracers = {}
+    for mode in ("1", "2", "0"):
+        monkeypatch.setenv("FOVRT_SHADE_HANDOFF", mode)
+        t = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=spp, dmd=3)
+        t.update_optix_variables(fovrt_mod.Camera.preset(1, W, H))
+        for _ in range(2):
+            t.geometry_launch(); t.sampling_launch(); t.optimize_launch(); t.shading_launch()
+        tracers[mode] = t
+    a, b, c = tracers["1"], tracers["2"], tracers["0"]
+    for tid in (TN.SHADING, TN.HISTORY_CACHE):
+        assert equal_nan(a.read(tid), b.read(tid)), tid
+    sa, sc = a.read(TN.SHADING), c.read(TN.SHADING)
+    assert np.array_equal(np.isnan(sa), np.isnan(sc))
+    assert (rmse_per_channel(sa, sc) <= 1e-6).all(), rmse_per_channel(sa, sc)
+    assert np.nanmax(np.abs(sa - sc)) <= 1e-4, mismatch_report(sa, sc)
+    st = [t.stats() for t in (a, b, c)]
+    for k in ("primary", "shadow", "mirror", "refraction", "reflection", "truncated"):
+        assert st[0][k] == st[1][k] == st[2][k], k
+    for t in (a, b, c):
+        t.destroy()
+
+
 @pytest.mark.parametrize("slots", ["3", "2"])
 def test_pipelined_frames_panning_equal_stage_calls(fovrt_mod, monkeypatch, slots):
     """fr_frame pipelining (front stages of frame N+1 beside entry 3 of frame N, reconstruction inputs and
