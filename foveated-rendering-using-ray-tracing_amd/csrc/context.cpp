@@ -28,7 +28,7 @@ void launch_sample_setup(const FrameUniforms&, const uint32_t*, const uint32_t*,
 void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
                           const f4*, unsigned long long*, f4*, f4*, uint32_t*, uint32_t, hipStream_t);
 size_t shade_counter_words();
-size_t shade_fx_slots(size_t slots, uint32_t handoff);
+size_t shade_fx_slots(uint32_t max_active, int spp, uint32_t handoff);
 void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
 void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
                      const f4*, f4*, uint8_t*, const uint8_t*, unsigned long long*, uint32_t*, int, uint8_t*, bool,
@@ -577,8 +577,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       dalloc(&c->tiles, 1024) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
       dalloc(&c->pull, atlas) != hipSuccess || dalloc(&c->push, atlas) != hipSuccess ||
       dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess ||
-      dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, std::max(N * cfg.spp, 2 * shade_fx_slots(N * cfg.spp, c->handoff))) != hipSuccess ||
-      dalloc(&c->sample_help, std::max<size_t>(4 * shade_fx_slots(N * cfg.spp, c->handoff), 1)) != hipSuccess ||
+      dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, std::max(N * cfg.spp, 2 * shade_fx_slots((uint32_t)N, cfg.spp, c->handoff))) != hipSuccess ||
+      dalloc(&c->sample_help, std::max<size_t>(4 * shade_fx_slots((uint32_t)N, cfg.spp, c->handoff), 1)) != hipSuccess ||
       dalloc(&c->aux, N) != hipSuccess || dalloc(&c->aux_seed, N) != hipSuccess ||
       (cfg.sibson_mode == 0 && (dalloc(&c->sib_prefix, (size_t)(c->W + 1) * c->H) != hipSuccess ||
                                 dalloc(&c->sib_blocks, (size_t)sibson_prefix_blocks(c->W) * c->H) != hipSuccess))) {

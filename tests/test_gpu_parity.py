@@ -345,8 +345,8 @@ def test_megakernel_schedule_does_not_change_samples(fovrt_mod, monkeypatch, chu
 def test_megakernel_tail_handoff(fovrt_mod, monkeypatch, W, H, spp):
     """The small-launch form of k_shade_paths (SampleSum): fixed-point sample sums, and idle lanes of a
     dry wave take pending refraction/reflection items of their busy neighbours. FOVRT_SHADE_HANDOFF=1 (the
-    default) uses it below 8 samples per lane, which covers 1080p and 256x256; 2 forces it, 0 turns it
-    off (fp32 running sums, the oracle's order). The default and the forced form are bit-identical
+    default) uses it for frames below 64 pixel-samples (W H spp) per lane of the grid, which covers 1080p
+    at 4 spp and 256x256; 2 forces it, 0 turns it off (fp32 running sums, the oracle's order). The default and the forced form are bit-identical
     (the same form; which lanes run an item does not change the integer sums); the fp32 form differs only
     by the rounding of the sums: per channel RMSE <= 1e-6, max 1e-4 on the tone-mapped colour."""
     monkeypatch.delenv("FOVRT_SHADE_CHUNK_REFR", raising=False)
