@@ -481,15 +481,18 @@ def test_cpp_facade_driver_matches_python(fovrt_mod, tmp_path):
 # unpacks the others' shading tiles and reconstructs; the composite equals the one-GPU frame.
 # Rehearsed here with three contexts on one device (one process), slabs in torch device memory.
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("nranks,tile,first,sparse", [(2, 64, 0, False), (3, 32, 0, False), (2, 64, 1, False),
-                                                     (3, 32, 1, False), (4, 16, 1, False), (3, 32, 0, True),
-                                                     (2, 64, 1, True), (4, 16, 1, True)])
-def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile, first, sparse):
+@pytest.mark.parametrize("nranks,tile,first,sparse,W,H", [(2, 64, 0, False, 200, 136), (3, 32, 0, False, 200, 136),
+                                                         (2, 64, 1, False, 200, 136), (3, 32, 1, False, 200, 136),
+                                                         (4, 16, 1, False, 200, 136), (3, 32, 0, True, 200, 136),
+                                                         (2, 64, 1, True, 200, 136), (4, 16, 1, True, 200, 136),
+                                                         (4, 128, 1, True, 3840, 2160)])
+def test_tile_shards_composite_equals_full_frame(fovrt_mod, nranks, tile, first, sparse, W, H):
     """first = 1 (fr_set_shard_ex, the bench default): the compositing rank traces no tiles. sparse: the
     gather sends only the traced pixels (fr_shard_pack_active / fr_shard_unpack_active) instead of the
-    ranks' tile slabs of SHADING."""
+    ranks' tile slabs of SHADING. 200x136 is not a multiple of the tiles (clipped border tiles); 4K is the
+    bench's tiling, where each tracer's launch is small but the frame is not: the sample-sum form follows
+    the frame size (SampleSum), so the ranks and the one-GPU frame still agree bit for bit."""
     import torch
-    W, H = 200, 136  # not multiples of the tile: clipped border tiles
     full = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
     ranks = [make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3) for _ in range(nranks)]
     for r, t in enumerate(ranks):
