@@ -138,6 +138,43 @@ def test_shading_within_tolerance(fovrt_mod, oracle, scene, spp, dmd, mask_mode,
     assert st["overflow"] == 0 and st["primary"] > 0
 
 
+@pytest.mark.parametrize("kind", ["empty", "last_pixel", "full", "one_row"])
+def test_shading_host_mask_edge_cases(fovrt_mod, oracle, kind):
+    """Entry 3 on a host-written mask (fr_write_buffer rebuilds the wave ballots): no active pixel (an empty
+    megakernel launch: every pixel carries its history), the last pixel alone (one partial wave, the end of
+    the active list), every pixel (the largest launch of the size) and one ragged row; two frames each, so
+    the second reprojects the first one's history. Against the oracle at the north-star tolerance."""
+    W, H, spp = 64, 48, 4
+    t = make_tracer(fovrt_mod, W, H, scene=1, mask=1, spp=spp, dmd=3)
+    uni = fovrt_mod.Camera.preset(1, W, H).uniforms(W, H)
+    t.set_camera_uniforms(uni)
+    osc = oracle.OracleScene(t.scene_arrays(), refraction_max_depth=16, diffuse_max_depth=3)
+    m = np.zeros((H, W), np.uint8)
+    if kind == "last_pixel":
+        m[H - 1, W - 1] = 1
+    elif kind == "full":
+        m[:] = 1
+    elif kind == "one_row":
+        m[H // 2, 3:W - 5] = 1
+    for _ in range(2):
+        frame = t.m_accumFrame
+        t.geometry_launch()
+        t.sampling_launch()
+        t.write(TN.MASK, m)
+        t.optimize_launch()
+        assert t.ray_count() == int(m.sum())
+        weight, hist_in = t.read(TN.WEIGHT), t.read(TN.HISTORY_CACHE)
+        t.shading_launch()
+        got = t.read(TN.SHADING)
+        ref = oracle.shading(osc, uni, W, H, frame, spp, m, weight, hist_in)
+        rm = rmse_per_channel(got, ref["shading"])
+        assert (rm <= 1e-3).all(), (kind, frame, rm, mismatch_report(got, ref["shading"]))
+        inactive = m == 0
+        assert equal_nan(t.read(TN.HISTORY_CACHE)[inactive], ref["history"][inactive])
+    st = t.stats()
+    assert st["overflow"] == 0 and (st["primary"] > 0) == (kind != "empty")
+
+
 @pytest.mark.parametrize("refr", [0, 1, 3])
 def test_shading_refraction_depth_cap(fovrt_mod, oracle, refr):
     """Glass bunny with the refraction recursion cut short (fr_config.refraction_max_depth): the
