@@ -455,11 +455,11 @@ def test_kernel_timing_counts_frames_and_leaves_results_unchanged(fovrt_mod):
         assert equal_nan(a.read(tid), b.read(tid)), tid
 
 
-@pytest.mark.parametrize("scene", [1, 2])
-def test_full_size_frame_properties(fovrt_mod, scene):
+@pytest.mark.parametrize("scene,W,H", [(1, 3840, 2160), (2, 3840, 2160), (1, 7680, 4320)])
+def test_full_size_frame_properties(fovrt_mod, scene, W, H):
     """BASELINE configs[2] (bunny) and the scene of configs[3] (vokselia) at full size (3840x2160, 4 spp,
-    GI 3, 10% log-polar mask): size-independent invariants of every stage."""
-    W, H = 3840, 2160
+    GI 3, 10% log-polar mask), and 8K (within the compaction scan's limit of 64 M pixels): size-independent
+    invariants of every stage."""
     t = make_tracer(fovrt_mod, W, H, scene=scene, mask=4, spp=4, dmd=3)
     for _ in range(2):
         tm = t.frame(timing=True)
