@@ -8,8 +8,10 @@ sampling mask -> compaction -> foveated path trace -> JumpFlooding -> Sibson -> 
 A-Trous, every stage a gfx950 HIP kernel behind the C ABI (include/fovrt.h).
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU, each rendering its own view (the eyes / views of a multi-view frame) with no data-path
-collective -> weak scaling; value = ray segments of all ranks / max elapsed over ranks.
+GPU; by default the one 4K view is tile-sharded over the N ranks (strong scaling) through libfovrt's
+multi-GPU group (fr_group_*: RCCL ncclSend/ncclRecv of the traced pixels to the two reconstruction
+ranks); --views N renders one view per rank instead (weak scaling). value = ray segments of all ranks
+(the G-buffer counted once per view) / max elapsed over ranks.
 
 Prints ONE JSON line (rank 0).
 """
@@ -92,8 +94,8 @@ def cpu_baseline(args, cfg_scene_arrays, cam_uni_fn):
 
 
 def view_offset(rank, world):
-    """Weak scaling over views: rank r renders its own eye/view, offset along x by 6.4 cm per view
-    around the preset camera (the stereo pair of BASELINE configs[4] at world 2)."""
+    """Views of a multi-view job: view v is an eye offset along x by 6.4 cm per view around the preset
+    camera (the stereo pair of BASELINE configs[4] at 2 views)."""
     return np.array([0.064 * (rank - (world - 1) / 2.0), 0.0, 0.0], np.float32)
 
 
@@ -112,8 +114,8 @@ def reduce_over_ranks(dist, device, elapsed, segs):
 
 def view_segments(st, G, vrank):
     """Ray segments a rank contributes to `value`, and its redundant ones. A tile-sharded view (G > 1)
-    traces its full G-buffer on every one of its G ranks (the saliency stencils and the root's A-Trous
-    read all of it): those W*H primaries count once per view, on the view's first rank; the other
+    traces its full G-buffer on every one of its G ranks (the saliency stencils and the reconstruction
+    ranks read all of it): those W*H primaries count once per view, on the view's first rank; the other
     ranks' copies are reported apart as redundant work, never as throughput."""
     segs = int(st["segments"])
     if G > 1 and vrank != 0:
@@ -122,46 +124,25 @@ def view_segments(st, G, vrank):
 
 
 def view_layout(rank, world, views):
-    """Ranks -> views: `views` views of world / views ranks each; the ranks of a view tile-shard it
-    and composite on the view's first rank. Returns (view, rank in view, ranks per view)."""
+    """Ranks -> views: `views` views of world / views ranks each (fr_group: rank r renders view r / G as
+    view rank r % G). Returns (view, rank in view, ranks per view)."""
     if views <= 0:
-        views = world
+        views = 1
     if world % views:
         raise SystemExit(f"--views {views} must divide the number of ranks {world}")
     g = world // views
     return rank // g, rank % g, g
 
 
-def make_view_groups(dist, world, views):
-    """One process group per view (every rank creates every group, in the same order)."""
-    g = world // views
-    return [dist.new_group(list(range(v * g, (v + 1) * g))) for v in range(views)]
-
-
-def gather_slabs(dist, group, slab, gather_list, dst):
-    """RCCL gather of every rank's packed tiles to the view's compositing rank `dst` (over gloo, as
-    in the one-GPU rehearsal, device slabs are staged through host memory)."""
-    if dist.get_backend() == "gloo" and slab.is_cuda:
-        host = slab.cpu()
-        hl = [t.cpu() for t in gather_list] if gather_list is not None else None
-        dist.gather(host, gather_list=hl, dst=dst, group=group)
-        if gather_list is not None:
-            for t, h in zip(gather_list, hl):
-                t.copy_(h)
-        return
-    dist.gather(slab, gather_list=gather_list, dst=dst, group=group)
-
-
-def allgather_slabs(dist, group, slab, out_list):
-    """All-gather of every rank's packed tiles (the moving-camera history exchange), staged through
-    host memory over gloo like gather_slabs."""
-    if dist.get_backend() == "gloo" and slab.is_cuda:
-        hl = [t.cpu() for t in out_list]
-        dist.all_gather(hl, slab.cpu(), group=group)
-        for t, h in zip(out_list, hl):
-            t.copy_(h)
-        return
-    dist.all_gather(out_list, slab, group=group)
+def broadcast_id(dist, rank, make_id):
+    """The 128-byte RCCL unique id of rank 0 (fr_rccl_unique_id) to every rank over the bootstrap
+    process group (gloo): the only use of torch.distributed besides the barrier and the reductions."""
+    import torch
+    t = torch.zeros(128, dtype=torch.uint8)
+    if rank == 0:
+        t.copy_(torch.frombuffer(bytearray(make_id()), dtype=torch.uint8))
+    dist.broadcast(t, 0)
+    return bytes(t.numpy().tobytes())
 
 
 def load_traffic(kernels, config):
@@ -198,25 +179,31 @@ def main():
     ap.add_argument("--refraction-max-depth", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-scale", type=int, default=1, help="CPU baseline at 1/scale resolution per axis")
-    ap.add_argument("--views", type=int, default=0,
-                    help="views rendered by the job (0: one per rank = weak scaling); the ranks of a view "
-                         "tile-shard it and gather the tiles to the view's first rank for reconstruction")
-    ap.add_argument("--tile", type=int, default=128, help="screen tile size of the tile sharding")
-    ap.add_argument("--dense-gather", action="store_true",
-                    help="tile sharding with a static camera: gather the ranks' whole tile slabs of SHADING instead "
-                         "of only the pixels they traced (the moving camera always uses the tile slabs)")
-    ap.add_argument("--root-traces", action="store_true",
-                    help="tile sharding: the view's compositing rank also traces tiles (default: its tiles go to "
-                         "the other ranks, and it runs the G-buffer and the reconstruction half only)")
+    ap.add_argument("--views", type=int, default=1,
+                    help="views rendered by the job (default 1: one 4K view tile-sharded over all ranks, strong "
+                         "scaling; --views N with N ranks: one view per rank, weak scaling)")
+    ap.add_argument("--tile", type=int, default=128, help="screen tile size of the tile sharding (multiple of 16)")
+    ap.add_argument("--no-split", action="store_true",
+                    help="both reconstruction chains on the view's rank 0 (default: JFA -> Sibson on view rank 0, "
+                         "pull-push -> A-Trous on view rank 1)")
+    ap.add_argument("--recon-cost", type=float, nargs=2, default=None,
+                    help="reconstruction work of view ranks 0 and 1 as fractions of a frame's trace work, for "
+                         "the tile dealing (default: fr_group_config_default's)")
     ap.add_argument("--composite", action="store_true",
-                    help="every frame, gather the views' reconstructed images to rank 0 over RCCL and compose them "
-                         "side by side (the final composite of the stereo configuration)")
+                    help="every frame, gather the views' A-Trous images to rank 0 over RCCL and lay them side by "
+                         "side (the final composite of the stereo configuration)")
+    ap.add_argument("--local-ranks", type=int, default=1,
+                    help="rehearsal on one device: this many ranks as contexts of one process (fr_group with "
+                         "device-to-device copies instead of RCCL); not a measurement of multi-GPU scaling")
     ap.add_argument("--bvh", default="host", choices=["host", "gpu"],
                     help="BVH builder: host binned SAH (default) or the GPU LBVH (k_bvh.hip)")
     ap.add_argument("--pan", type=float, default=0.0,
                     help="per-frame step of the camera's look-at target in scene units (0: static camera). A "
-                         "moving camera makes the history reprojection read across tiles; tile-sharded views "
-                         "then all-gather HISTORY_CACHE every frame")
+                         "moving camera makes the history reprojection read across tiles; every rank of a "
+                         "tile-sharded view then receives every other rank's traced pixels")
+    ap.add_argument("--gaze-path", action="store_true",
+                    help="the gaze follows a scripted cursor path every frame (cursorPosCallback, FR/gui.cpp:48-66): "
+                         "the log-polar mask is recomputed every frame (an eye-tracked frame)")
     args = ap.parse_args()
     args.mask = fovrt.MASKS[args.mask]
     scene = fovrt.SCENES[args.scene]
@@ -227,13 +214,14 @@ def main():
     import torch
     dist = None
     if world > 1:
+        # torch.distributed (gloo, CPU) is the bootstrap only: the RCCL id, barriers, max/sum reductions.
+        # Every frame's data path is libfovrt's own RCCL group (fr_group_*).
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("FOVRT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
-        if backend == "nccl":
-            torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend=backend)
+        dist.init_process_group(backend="gloo")
     has_gpu = torch.cuda.is_available()
+    if world > 1 and args.local_ranks > 1:
+        raise SystemExit("--local-ranks is a one-process rehearsal; do not combine it with torch.distributed")
 
     def sync():
         if has_gpu:
@@ -244,185 +232,135 @@ def main():
             dist.barrier()
 
     W, H = args.width, args.height
-    # one GPU per rank; more ranks than GPUs (the gloo rehearsal on a one-GPU box) share them
     ndev = max(1, torch.cuda.device_count())
-    device = local_rank % ndev
-    views = args.views or world
-    view, vrank, G = view_layout(rank, world, views)
-    groups = make_view_groups(dist, world, views) if dist is not None and G > 1 else None
-    # the first rank of every view, for the final composite on rank 0
-    roots_group = (dist.new_group([v * (world // views) for v in range(views)])
-                   if dist is not None and args.composite and views > 1 else None)
-    cfg = fovrt.Config(width=W, height=H, scene=scene, mask_mode=args.mask, spp=args.spp, diffuse_max_depth=args.dmd,
-                       refraction_max_depth=args.refraction_max_depth, device=device,
-                       bvh_builder=1 if args.bvh == "gpu" else 0)
-    tracer = fovrt.PathTracer(cfg)
-    tracer.initialize()
-    cam = fovrt.Camera.preset(scene, W, H)
-    # each view is its own eye/camera (offset along x, 6.4 cm per view)
-    if views > 1:
-        cam.setPosition(np.asarray(cam.pos) + view_offset(view, views))
-        cam.lookAt(cam.target)
-    tracer.update_optix_variables(cam)
+    R = world if world > 1 else args.local_ranks   # ranks of the group
+    views = args.views
+    my_ranks = [rank] if world > 1 else list(range(R))
+    layouts = [view_layout(r, R, views) for r in my_ranks]
+    G = layouts[0][2]
+    cfg_kw = dict(width=W, height=H, scene=scene, mask_mode=args.mask, spp=args.spp, diffuse_max_depth=args.dmd,
+                  refraction_max_depth=args.refraction_max_depth, bvh_builder=1 if args.bvh == "gpu" else 0)
+    tracers = []
+    for r in my_ranks:
+        t = fovrt.PathTracer(fovrt.Config(device=(local_rank if world > 1 else 0) % ndev, **cfg_kw))
+        t.initialize()
+        tracers.append(t)
+    tracer = tracers[0]
+    cams = {}
+    for (view, _, _), t in zip(layouts, tracers):
+        if view not in cams:
+            cam = fovrt.Camera.preset(scene, W, H)
+            if views > 1:  # each view is its own eye (offset along x, 6.4 cm per view)
+                cam.setPosition(np.asarray(cam.pos) + view_offset(view, views))
+                cam.lookAt(cam.target)
+            cams[view] = cam
+        t.update_optix_variables(cams[view])
 
-    slab = gather_list = None
-    if G > 1:
-        # the compositing rank runs the reconstruction half, which no other rank can share (JFA's
-        # reach, the global pull-push pyramid): by default it traces no tiles (fr_set_shard_ex)
-        first_tracer = 0 if args.root_traces else 1
-        tracer.set_shard(vrank, G, args.tile, first_tracer)
-        n_tex = tracer.shard_texels()
-        slab = torch.empty(n_tex * 4, dtype=torch.float32, device=f"cuda:{device}")
-        if vrank == 0:
-            gather_list = [torch.empty_like(slab) for _ in range(G)]
-        nbytes = n_tex * 16
-        root = view * G
-        if args.pan:
-            hist_slab = torch.empty_like(slab)
-            hist_list = [torch.empty_like(slab) for _ in range(G)]
-        # sparse gather (static camera): the traced pixels only, 20 B each (fr_shard_pack_active); a rank
-        # traces at most its tiles' pixels, so n_tex entries always fit
-        sparse = not args.pan and not args.dense_gather
-        if sparse:
-            act = torch.empty(n_tex * 5, dtype=torch.float32, device=f"cuda:{device}")
-            act_list = [torch.empty_like(act) for _ in range(G)] if vrank == 0 else None
-            cnt_t = torch.zeros(1, dtype=torch.int64, device=f"cuda:{device}")
-            cnt_list = [torch.zeros_like(cnt_t) for _ in range(G)]
-
-    comp_img = comp_list = comp_out = None
-    if roots_group is not None and vrank == 0:
-        comp_img = torch.empty(W * H * 4, dtype=torch.float32, device=f"cuda:{device}")
-        if rank == 0:
-            comp_stack = torch.empty(views * W * H * 4, dtype=torch.float32, device=f"cuda:{device}")
-            comp_list = list(comp_stack.chunk(views))  # the gather lands the views consecutively
-            comp_out = torch.empty_like(comp_stack)
-
-    def composite():
-        """Final composite: view roots send their A-Trous image to rank 0, which lays them side by side."""
-        if comp_img is None:
-            return
-        tracer.copy_buffer(fovrt.TextureName.ATROUS, comp_img.data_ptr(), W * H * 16)
-        gather_slabs(dist, roots_group, comp_img, comp_list, 0)
-        if rank == 0:
-            sync()
-            tracer.composite_views(comp_list[0].data_ptr(), views, comp_out.data_ptr(), comp_out.numel() * 4)
-
-    def step(timing):
-        """One frame of the view: the whole chain on one rank, or trace -> pack -> gather -> (root)
-        unpack + reconstruct when the view is tile-sharded; then the optional final composite."""
-        if args.pan:
-            move_camera()
-        tm = view_frame(timing)
-        composite()
-        return tm
+    group = None
+    if R > 1:
+        gkw = dict(views=views, tile=args.tile, split_recon=not args.no_split, moving_camera=args.pan != 0.0,
+                   composite=args.composite and views > 1, recon_cost=args.recon_cost)
+        if world > 1:
+            uid = broadcast_id(dist, rank, fovrt.rccl_unique_id)
+            group = fovrt.Group.rccl(tracer, uid, world, rank, **gkw)
+        else:
+            group = fovrt.Group(tracers, **gkw)
+    roles = [group.rank_info(i) for i in range(len(tracers))] if group else [{"view": 0, "view_rank": 0, "chains": 3,
+                                                                             "tiles": -1}]
 
     step_dir = np.array([1.0, 0.5, 0.0], np.float32)
     step_dir *= np.float32(args.pan) / np.linalg.norm(step_dir)
+    frame_no = [0]
 
     def move_camera():
         """Camera path of the moving-camera runs: the eye stays, the look-at target moves a fixed step per
-        frame (setPrevState first, so frame N reprojects into frame N-1 as FR/main.cpp:357 does)."""
-        cam.setPrevState()
-        cam.lookAt(np.asarray(cam.target) + step_dir)
-        tracer.update_optix_variables(cam)
+        frame (setPrevState first, so frame N reprojects into frame N-1 as FR/main.cpp:443 does)."""
+        for cam in cams.values():
+            cam.setPrevState()
+            cam.lookAt(np.asarray(cam.target) + step_dir)
+        for (view, _, _), t in zip(layouts, tracers):
+            t.update_optix_variables(cams[view])
 
-    def exchange_history():
-        """Reprojection reads the previous frame's history anywhere on the screen, so with a moving camera
-        every rank of a view needs the others' tiles of HISTORY_CACHE before its next trace."""
-        tracer.shard_pack(fovrt.TextureName.HISTORY_CACHE, hist_slab.data_ptr(), nbytes)
-        allgather_slabs(dist, groups[view], hist_slab, hist_list)
-        sync()
-        for r in range(G):
-            if r != vrank:
-                tracer.shard_unpack(fovrt.TextureName.HISTORY_CACHE, r, hist_list[r].data_ptr(), nbytes)
+    def move_gaze():
+        """A scripted cursor (window coordinates, y down) circling the screen centre at a quarter of the
+        height, one degree per frame, fed through cursorPosCallback's mapping (fr_set_gaze, windowed)."""
+        a = np.deg2rad(frame_no[0])
+        x = W / 2 + 0.25 * H * np.cos(a)
+        y = (H / 2 + 0.25 * H * np.sin(a)) / 1.25  # the callback scales y by 1.25 in a window
+        for t in tracers:
+            t.set_gaze(x, y)
 
-    def view_frame(timing):
-        if G == 1:
-            return tracer.frame(timing=timing)
-        tm = tracer.trace_frame(timing=timing)
+    def step(timing):
         if args.pan:
-            exchange_history()
-        sync()  # the previous frame's gather of `slab` has finished on torch's stream
-        if sparse:
-            cnt_t.fill_(tracer.ray_count())
-            allgather_slabs(dist, groups[view], cnt_t, cnt_list)
-            counts = [int(c.item()) for c in cnt_list]
-            cap = max(max(counts), 1)
-            n_packed = tracer.shard_pack_active(act.data_ptr(), cap)
-            assert n_packed == counts[vrank]
-            gather_slabs(dist, groups[view], act[:cap * 5],
-                         [a[:cap * 5] for a in act_list] if act_list is not None else None, root)
-            if vrank == 0:
-                sync()
-                for r in range(1, G):
-                    tracer.shard_unpack_active(act_list[r].data_ptr(), cap, counts[r])
-        else:
-            tracer.shard_pack(fovrt.TextureName.SHADING, slab.data_ptr(), nbytes)
-            gather_slabs(dist, groups[view], slab, gather_list, root)
-        if vrank == 0:
-            sync()
-            if not sparse:
-                for r in range(1, G):
-                    tracer.shard_unpack(fovrt.TextureName.SHADING, r, gather_list[r].data_ptr(), nbytes)
-            rec = tracer.reconstruct_frame(timing=timing)
-            if timing:
-                for k in ("jfa_ms", "sibson_ms", "pullpush_ms", "atrous_ms"):
-                    tm[k] = rec[k]
-        return tm
+            move_camera()
+        if args.gaze_path:
+            move_gaze()
+        frame_no[0] += 1
+        if group is None:
+            return tracer.frame(timing=timing)
+        tm = group.frame(timing=timing)
+        return tm[0] if timing else None
 
     for _ in range(args.warmup):
         step(False)
-    tracer.synchronize()
+    if group:
+        group.synchronize()
+    for t in tracers:
+        t.synchronize()
     sync()
-    tracer.reset_stats()
+    for t in tracers:
+        t.reset_stats()
 
-    # The timed region: K frames enqueued back to back. fr_frame pipelines them: frame N's
-    # reconstruction (JFA/Sibson and pull-push/A-Trous streams) runs while frame N+1 traces.
-    # entry 3 (the roofline stage) is timed live inside the timed region: HIP events on the context
-    # stream around the stage and its megakernel, recorded by the library, no synchronisation added
+    # The timed region: K frames enqueued back to back; consecutive frames pipeline (frame N's
+    # reconstruction runs while frame N+1 traces). Entry 3 (the roofline stage) is timed live inside it:
+    # HIP events on the context stream around the stage and its megakernel, no synchronisation added.
     tracer.kernel_timing(True)
     barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(False)
-    tracer.synchronize()
+    if group:
+        group.synchronize()
+    for t in tracers:
+        t.synchronize()
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
     live = tracer.kernel_times()
     tracer.kernel_timing(False)
 
+    segs = redundant = 0
+    for (view, vrank, g), t in zip(layouts, tracers):
+        a, b = view_segments(t.stats(), g, vrank)
+        segs += a
+        redundant += b
     st = tracer.stats()
-    segs, redundant = view_segments(st, G, vrank)
-    dev = None
-    if dist is not None:
-        dev = torch.device("cuda", device) if has_gpu and dist.get_backend() == "nccl" else torch.device("cpu")
+    dev = torch.device("cpu") if dist is not None else None
     elapsed, total_segs = reduce_over_ranks(dist, dev, elapsed, segs)
     _, total_redundant = reduce_over_ranks(dist, dev, 0.0, redundant)
 
     # Per-stage HIP-event breakdown of the same frames, serialised (each frame synchronised, so the
     # stage times do not overlap the next frame): the stage table and the roofline kernel time.
     stage_ms = {}
-    ray_counts = []
     n_timed = max(3, min(args.steps, 10))
     for _ in range(n_timed):
         tm = step(True)
         for k, v in tm.items():
             if k.endswith("_ms"):
                 stage_ms[k] = stage_ms.get(k, 0.0) + v
-        ray_counts.append(tm["ray_count"])
-    tracer.synchronize()
+    for t in tracers:
+        t.synchronize()
+    # foveal density: every rank's active pixels of the last frame (a rank traces only its tiles)
+    count_sum = float(sum(t.ray_count() for t in tracers))
+    _, count_sum = reduce_over_ranks(dist, dev, 0.0, count_sum)
 
     K = args.steps
     avg = {k[:-3]: v / n_timed for k, v in stage_ms.items()}
-    # foveal density: the active pixels of all ranks of all views (a tile-sharded view's ranks each trace
-    # a part; with first_tracer 1 the compositing rank traces none)
-    _, count_sum = reduce_over_ranks(dist, dev, 0.0, float(np.mean(ray_counts)))
     rho = count_sum / views / (W * H)
     L = jfa_passes(W, H)
     sb = stage_bytes(W, H, rho, args.spp, L)
-    # (a non-compositing rank of a tile-sharded view runs no reconstruction: its image stages are 0 ms)
+    # (a rank that runs no reconstruction chain reports 0 ms for those stages)
     stage_table = {k: {"ms": round(avg[k], 4),
                        "GB/s": round(sb[k] / (avg[k] * 1e-3) / 1e9, 1) if avg[k] > 0 else None} for k in sb}
     # the dominant stage is entry 3 (shading_launch): k_shade_paths (path-trace megakernel) +
@@ -442,6 +380,19 @@ def main():
     image_stages = ["sampling", "optimize", "jfa", "sibson", "pullpush", "atrous"]
     img_bytes = sum(sb[k] for k in image_stages)
     img_ms = sum(avg[k] for k in image_stages)
+    n_ranks = R
+    if R == 1:
+        parallelism = "one view on one GPU"
+    elif G == 1:
+        parallelism = f"{views} views, one per rank (weak scaling), no data-path collective"
+    else:
+        parallelism = (f"{views} view(s) x {G}-way {args.tile}px tile sharding (fr_group, tiles dealt by reconstruction "
+                       f"load); traced pixels (20 B each) to the view's reconstruction ranks over RCCL "
+                       f"ncclSend/ncclRecv; " + ("both chains on view rank 0" if args.no_split else
+                                                 "JFA -> Sibson on view rank 0, pull-push -> A-Trous on view rank 1") +
+                       (" (every rank receives every rank's pixels: moving camera)" if args.pan else ""))
+    if args.local_ranks > 1:
+        parallelism += f"; REHEARSAL: {R} ranks as contexts of one process on one device (not a scaling measurement)"
     result = {
         "metric": "Mrays/s + reconstructed fps @4K, 10% foveal density, 1/2/4/8 GPU",
         "value": round(total_segs / elapsed / 1e6, 3),
@@ -459,14 +410,10 @@ def main():
                                f"log-polar mask ({'signed, ~10%' if args.mask == 4 else 'mode %d' % args.mask}), "
                                "JFA + Sibson + pull-push + A-Trous",
                    "scene": args.scene, "width": W, "height": H, "spp": args.spp, "diffuse_max_depth": args.dmd,
-                   "mask_mode": args.mask, "foveal_density": round(rho, 5), "views": views,
+                   "mask_mode": args.mask, "foveal_density": round(rho, 5), "views": views, "ranks": n_ranks,
                    "composite": bool(args.composite and views > 1), "camera_step": args.pan,
-                   "parallelism": (f"views x{world} (one view per GPU)" if G == 1 else
-                                   f"{views} view(s) x {G}-way {args.tile}px tile sharding, RCCL gather to the "
-                                   f"view's first rank" + ("" if args.root_traces else
-                                                          ", which traces no tiles and reconstructs") +
-                                   (" (tile slabs of SHADING)" if args.pan or args.dense_gather else
-                                    " (only the traced pixels, 20 B each)")),
+                   "gaze": "scripted cursor path, mask recomputed every frame" if args.gaze_path else "screen centre",
+                   "parallelism": parallelism,
                    "procedural_meshes": "box/bunny/earth stand-ins (the reference's .obj files are absent)"},
         "fps": round(K / elapsed, 2),
         "frames_per_s_total": round(views * K / elapsed, 2),
@@ -474,9 +421,10 @@ def main():
                                     "refraction", "reflection", "truncated", "overflow")},
         "rays_note": "rank 0's counters over the timed frames",
         "gbuffer_redundant_segments": int(total_redundant),
+        "rank0_role": roles[0],
         "stages": stage_table,
-        "stages_note": f"HIP events, {n_timed} serialised frames; the timed region pipelines frame N's reconstruction "
-                       "with frame N+1's trace half, so ms_per_step < the sum of the stages",
+        "stages_note": f"rank 0's HIP events, {n_timed} serialised frames; the timed region pipelines frame N's "
+                       "reconstruction with frame N+1's trace half, so ms_per_step < the sum of the stages",
         "roofline": {"bound": "hbm", "kernel": f"{dominant} stage ({' + '.join(stage_kernels.get(dominant, []))})",
                      "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": None,
@@ -493,16 +441,18 @@ def main():
                                   "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                   "frac": round(img_bytes / (img_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)},
     }
-    traffic, src = load_traffic(stage_kernels.get(dominant, []), result["config"])
+    traffic, src = load_traffic(stage_kernels.get(dominant, []), result["config"]) if R == 1 else (None, None)
     if traffic is not None:
         result["roofline"]["traffic"] = int(traffic)
         result["roofline"]["traffic_source"] = src
         result["roofline"]["measured_hbm_GBs"] = round(traffic / (launch_ms * 1e-3) / 1e9, 1)
+    if group:
+        group.destroy()
     # the GPU BVH builder on this scene (after every measurement: it replaces the BVH)
     builds = sorted(tracer.rebuild_bvh() for _ in range(3))
     result["bvh"] = {"builder": args.bvh, "gpu_rebuild_ms": round(builds[1], 3),
                      "triangles": int(tracer.scene_arrays()["pos"].shape[0])}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and R == 1 and not args.no_cpu_baseline:
         try:
             arrays = tracer.scene_arrays()
 
@@ -513,7 +463,8 @@ def main():
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:
         print(json.dumps(result), flush=True)
-    tracer.destroy()
+    for t in tracers:
+        t.destroy()
     if dist is not None:
         dist.destroy_process_group()
 

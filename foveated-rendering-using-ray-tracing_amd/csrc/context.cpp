@@ -14,156 +14,11 @@
 #include <vector>
 
 #include <chrono>
-#include "../../include/fovrt.h"
-#include "fr_device.h"
-#include "scene.h"
-
-namespace fr {
-void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
-void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
-                        const f4*, uint32_t*, f4*, unsigned long long*, DevStats*, f4*, uint32_t*, uint32_t, uint32_t,
-                        uint32_t, hipStream_t);
-void launch_sample_setup(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*, f4*,
-                         uint32_t*, hipStream_t);
-void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
-                          const f4*, unsigned long long*, f4*, f4*, uint32_t*, uint32_t, hipStream_t);
-size_t shade_counter_words();
-size_t shade_fx_slots(uint32_t max_active, int spp, uint32_t handoff);
-void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
-void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
-                     const f4*, f4*, uint8_t*, const uint8_t*, unsigned long long*, uint32_t*, int, uint8_t*, bool,
-                     hipStream_t);
-void launch_mask_words(const uint8_t*, const uint8_t*, int, int, unsigned long long*, uint32_t*, hipStream_t);
-void launch_compaction(int, int, const unsigned long long*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
-                       uint32_t*, hipStream_t);
-size_t compaction_tiles(int W, int H);
-void launch_shard_pack(const FrameUniforms&, const f4*, f4*, hipStream_t);
-void launch_logpolar(const f4*, f4*, f4*, int, int, f2, hipStream_t);
-void launch_composite(const f4*, int, int, int, f4*, hipStream_t);
-void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
-void launch_shard_pack_active(const uint32_t*, const uint32_t*, uint32_t, const f4*, f4*, uint32_t*, hipStream_t);
-void launch_shard_unpack_active(const f4*, const uint32_t*, uint32_t, f4*, f4*, hipStream_t);
-void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, hipStream_t);
-void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
-void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, int, int, hipStream_t);
-int sibson_prefix_blocks(int W);
-bool gpu_build_bvh(const f3*, int, BvhNode**, TriGeo**, int32_t**, int*, int*, hipStream_t, std::string&);
-#ifdef FR_STAMPS
-void launch_trace_queries(const DevScene&, const f4*, uint32_t, f4*, uint32_t*, hipStream_t, int);
-void diag_record_queries(f4*, uint32_t, hipStream_t);
-uint32_t diag_recorded_queries(hipStream_t);
-void diag_sample_trace(uint32_t*, uint32_t, uint32_t*, uint32_t, hipStream_t);
-#endif
-void launch_pullpush(const f4*, f4*, f4*, f4*, f4*, int, int, hipStream_t);
-void launch_atrous(const f4*, const f4*, const f4*, f4*, int, int, float, float, float, float, hipStream_t);
-int pp_size(int W, int H);
-size_t pp_snap_count(int S);
-}  // namespace fr
+#include "ctx_internal.h"
 
 using namespace fr;
 
 static thread_local std::string g_create_error;
-
-enum Phys {
-  P_POSITION, P_NORMAL, P_DEPTH_A, P_DEPTH_B, P_DIFFUSE, P_WEIGHT, P_HIST_A, P_HIST_B, P_SHADING, P_EXTRA,
-  P_JFA_COORD, P_JFA_COLOR, P_SIBSON, P_PULLPUSH, P_ATROUS_A, P_ATROUS_B, P_LOGPOLAR, P_LOGPOLAR_INV,
-  // frame-slot copies of the buffers the reconstruction reads (POSITION, NORMAL, SHADING) and of
-  // WEIGHT (read by the trace half's tail); slot 0 is the plain entry above
-  P_POSITION_B, P_NORMAL_B, P_SHADING_B, P_WEIGHT_B,
-  P_POSITION_C, P_NORMAL_C, P_SHADING_C, P_WEIGHT_C,
-  P_COUNT
-};
-
-struct fr_ctx {
-  fr_config cfg;
-  std::string asset_dir;
-  std::string err;
-  int W = 0, H = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // reconstruction chain 2: pull-push -> A-Trous
-  hipStream_t stream3 = nullptr;  // reconstruction chain 1: JFA -> Sibson
-  hipStream_t stream4 = nullptr;  // entry 3's carry of the inactive pixels, beside the megakernel
-  hipStream_t stream5 = nullptr;  // front stages of a pipelined frame (entries 0-2), beside the previous megakernel
-  // Frame pipelining: frame N's reconstruction (stream3 + stream2) runs while later frames trace.
-  // The buffers the reconstruction reads (POSITION, NORMAL, SHADING) rotate over `nslots` frame
-  // slots (`slot` = the current frame's); a frame's front stages wait for the reconstruction that
-  // last read their slot (ev_recon). The front stages of a pipelined frame (G-buffer, sampling,
-  // compaction) run on stream5 while the previous frame's megakernel still runs on `stream`: they
-  // read nothing entry 3 writes. What entry 3's tail reads of them (WEIGHT, mask, active list, ray
-  // count) rotates with the slot as well; the front of a frame waits for the trace half that last
-  // read its slot (ev_trace), and entry 3 of a frame waits for its own front (ev_front).
-  static constexpr int MAX_SLOTS = 3;
-  int nslots = 3;
-  int slot = 0;
-  bool recon_pending[MAX_SLOTS] = {};
-  bool front_pending = false;
-  bool trace_pending[MAX_SLOTS] = {};
-  hipEvent_t ev_front = nullptr, ev_trace[MAX_SLOTS] = {}, ev_recon[MAX_SLOTS] = {};
-  uint8_t* mask_p[MAX_SLOTS] = {};
-  uint32_t* active_p[MAX_SLOTS] = {};
-  uint32_t* ray_count_p[MAX_SLOTS] = {};
-  HostScene scene;
-  Bvh bvh;
-  // device scene
-  BvhNode* d_nodes = nullptr;
-  f3* d_pos = nullptr;  // world-space vertices, 3 per triangle (the GPU builder's input)
-  TriGeo* d_tri = nullptr;
-  int32_t* d_prim = nullptr;
-  TriShade* d_shade = nullptr;
-  std::vector<f4*> d_tex;
-  DevMaterial* d_mats = nullptr;
-  DevTexture* d_texs = nullptr;
-  DevScene dsc;
-  // image buffers
-  f4* img[P_COUNT] = {};
-  int depth_cur = P_DEPTH_A, depth_cache = P_DEPTH_B;
-  int hist_cur = P_HIST_A, hist_cache = P_HIST_B;
-  int atrous_out = P_ATROUS_A;
-  uint8_t* mask = nullptr;  // mask_p[slot]
-  uint8_t* gclass = nullptr;
-  uint8_t* lp_cache = nullptr;  // log-polar mask for (lp_gaze, lp_mode); recomputed when either changes
-  f2 lp_gaze{-1e30f, -1e30f};
-  int lp_mode = -1;
-  unsigned long long* words = nullptr;
-  uint32_t* counts = nullptr;
-  uint32_t* offsets = nullptr;  // per (class, block) local prefix
-  uint32_t* tiles = nullptr;
-  uint32_t* ray_count = nullptr;  // ray_count_p[slot]
-  uint32_t* active = nullptr;     // active_p[slot]
-  uint32_t* shade_ctr = nullptr;  // sharded chunk counters of the shading work queue
-  f4* samples = nullptr;          // one radiance value per (active pixel, camera sample): 16 B, or 32 B fixed point
-  unsigned long long* sample_help = nullptr;  // fixed-point shares of the lanes that took over items, 32 B per sample
-  f4* aux = nullptr;              // per active pixel: NDC position, r1, r2 (k_sample_setup)
-  uint32_t* aux_seed = nullptr;   // per active pixel: the seed after the two draws
-  u2 *jfa_a = nullptr, *jfa_b = nullptr;  // JFA state ping-pong (seed coord texel + alpha flags)
-  uint32_t chunk_refr = 0;  // fixed refraction-class chunk of the megakernel (FOVRT_SHADE_CHUNK_REFR), 0 adaptive
-  uint32_t xcd_bands = 1;   // megakernel queue: per-XCD class bands (FOVRT_SHADE_XCD_BANDS=0: interleaved chunks)
-  uint32_t handoff = 1;     // megakernel tail handoff (FOVRT_SHADE_HANDOFF): 0 never, 1 small launches, 2 always
-  float* ftab = nullptr;  // texel-centre coordinates ((x + 0.5) / W, x < W; then (y + 0.5) / H)
-  f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
-  f4 *sib_prefix = nullptr, *sib_blocks = nullptr;  // Sibson run form: per-row block prefix sums + block totals
-  int pp_S = 0;
-  DevStats* stats = nullptr;
-  FrameUniforms U;
-  uint32_t accum = 0;
-  bool light_pending = false;
-  bool compacted = false;
-  bool mask_dirty = false;
-  hipEvent_t ev[24] = {};  // 0-15 stage timing; 16 fork; 17 chain-2 join; 20-22 chain-1 timing
-  bool time_kernels = false;  // fr_frame with timing: also time the path-trace kernel alone
-  // Live timing of entry 3 inside pipelined (untimed) frames: a ring of event quadruples recorded on
-  // the context stream around carry_history / k_shade_paths / resolve (fr_kernel_timing); a slot is
-  // harvested (its elapsed times summed) before it is reused and by fr_kernel_times.
-  static constexpr int KT_RING = 32;
-  hipEvent_t kt_ev[KT_RING][4] = {};
-  bool kt_on = false;
-  int kt_next = 0, kt_pending = 0;
-  uint32_t kt_frames = 0;
-  double kt_stage_ms = 0.0, kt_kernel_ms = 0.0;
-  // scene export copies
-  std::vector<const float*> tex_ptrs;
-  std::vector<int32_t> tex_dims, mat_pairs;
-};
 
 namespace {
 
@@ -311,11 +166,13 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
 // ---------------------------------------------------------------------------------------------
 extern "C" {
 
-const char* fr_version(void) { return "fovrt 0.1 (gfx950)"; }
+const char* fr_version(void) { return "fovrt 0.2 (gfx950)"; }
+int fr_abi_version(void) { return FOVRT_ABI_VERSION; }
 
 int fr_config_default(fr_config* c) {
   if (!c) return FR_E_INVALID;
   memset(c, 0, sizeof(*c));
+  c->abi_version = FOVRT_ABI_VERSION;
   c->width = 1024; c->height = 1024;
   c->scene = FR_SCENE_BUNNY;
   c->mask_mode = FR_MASK_SALIENCY;
@@ -444,6 +301,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   *out = nullptr;
   fr_config cfg;
   if (cfg_in) cfg = *cfg_in; else fr_config_default(&cfg);
+  if (cfg.abi_version != FOVRT_ABI_VERSION)
+    return fail(nullptr, FR_E_INVALID, "fr_config.abi_version != FOVRT_ABI_VERSION (initialise it with fr_config_default)");
   if (cfg.width <= 0 || cfg.height <= 0 || cfg.width > 32767 || cfg.height > 32767)
     return fail(nullptr, FR_E_INVALID, "width/height out of range (1..32767)");
   if (!(cfg.spp == 1 || cfg.spp == 2 || cfg.spp == 4 || cfg.spp == 8))
@@ -488,6 +347,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   hipEventCreateWithFlags(&c->ev_front, hipEventDisableTiming);
   for (auto& e : c->ev_trace) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->ev_recon) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& e : c->ev_counts) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (const char* v = getenv("FOVRT_SHADE_CHUNK_REFR")) c->chunk_refr = (uint32_t)std::max(0, atoi(v));
   if (const char* v = getenv("FOVRT_SHADE_XCD_BANDS")) c->xcd_bands = atoi(v) != 0;
   if (const char* v = getenv("FOVRT_SHADE_HANDOFF")) c->handoff = (uint32_t)std::min(std::max(atoi(v), 0), 2);
@@ -572,6 +432,16 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       return bail(FR_E_NOMEM);
     }
   c->mask = c->mask_p[0]; c->ray_count = c->ray_count_p[0]; c->active = c->active_p[0];
+  for (int k = 0; k < fr_ctx::MAX_SLOTS; k++)
+    if (dalloc(&c->owner_counts_p[k], FR_MAX_SHARD_RANKS) != hipSuccess) {
+      c->err = "device allocation (work buffers) failed";
+      return bail(FR_E_NOMEM);
+    }
+  if (dalloc(&c->bcount, nblocks) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_counts, sizeof(uint32_t) * fr_ctx::MAX_SLOTS * FR_MAX_SHARD_RANKS) != hipSuccess) {
+    c->err = "allocation (shard counts) failed";
+    return bail(FR_E_NOMEM);
+  }
   if (dalloc(&c->gclass, N) != hipSuccess || dalloc(&c->lp_cache, N) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
       dalloc(&c->counts, 4 * nblocks) != hipSuccess || dalloc(&c->offsets, 4 * nblocks) != hipSuccess ||
       dalloc(&c->tiles, 1024) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
@@ -602,7 +472,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   U.spp = cfg.spp;
   U.sqrt_spp = (int)floor(sqrt((double)cfg.spp) + 1e-9);
   U.mask_mode = cfg.mask_mode;
-  U.shard_rank = 0; U.shard_count = 1; U.shard_tile = 128; U.shard_tiles_x = (c->W + 127) / 128; U.shard_first = 0;
+  U.shard_rank = 0; U.shard_count = 1; U.shard_tile = 128; U.shard_tiles_x = (c->W + 127) / 128; U.shard_map = nullptr;
   {
     fr_camera_pose pose;
     float eye[3], tgt[3], upv[3] = {0, 1, 0};
@@ -634,7 +504,10 @@ int fr_destroy(fr_ctx* c) {
   for (auto p : c->d_tex) fr(p);
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
-  for (int k = 0; k < fr_ctx::MAX_SLOTS; k++) { fr(c->mask_p[k]); fr(c->ray_count_p[k]); fr(c->active_p[k]); }
+  for (int k = 0; k < fr_ctx::MAX_SLOTS; k++) { fr(c->mask_p[k]); fr(c->ray_count_p[k]); fr(c->active_p[k]); fr(c->owner_counts_p[k]); }
+  fr(c->bcount); fr(c->shard_map);
+  if (c->h_counts) hipHostFree(c->h_counts);
+  for (auto e : c->ev_counts) if (e) hipEventDestroy(e);
   fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
@@ -698,6 +571,7 @@ static int P_wgt(const fr_ctx* c) { return slotted(c, P_WEIGHT, P_WEIGHT_B); }
 // The context stream waits for every reconstruction still in flight (before any call that reads or
 // writes what the reconstruction uses, or hands buffers to the caller).
 static void join_recon(fr_ctx* c) {
+  c->stream_dirty = true;  // the caller is about to enqueue on `stream` outside a pipelined frame
   for (int k = 0; k < fr_ctx::MAX_SLOTS; k++)
     if (c->recon_pending[k]) { hipStreamWaitEvent(c->stream, c->ev_recon[k], 0); c->recon_pending[k] = false; }
   if (c->front_pending) { hipStreamWaitEvent(c->stream, c->ev_front, 0); c->front_pending = false; }
@@ -739,7 +613,15 @@ static int enqueue_sampling(fr_ctx* c, hipStream_t fs) {
   if (lp_refresh) { c->lp_mode = c->U.mask_mode; c->lp_gaze = c->U.gaze; }
   launch_sampling(c->U, c->dsc, c->img[P_pos(c)], c->img[c->depth_cur], c->img[c->depth_cache], c->img[P_wgt(c)],
                   c->img[P_nrm(c)], c->img[P_DIFFUSE], c->img[P_EXTRA], c->mask, c->gclass, c->words, c->counts,
-                  c->cfg.write_extra, c->lp_cache, lp_refresh, fs);
+                  c->cfg.write_extra, c->lp_cache, lp_refresh, c->U.shard_count > 1 ? c->bcount : nullptr, fs);
+  if (c->U.shard_count > 1) {
+    // every rank's active count of this frame (fr_shard_counts, the group's transfer sizes), to pinned
+    // host memory with its own event: reading it waits for this frame's front stages only
+    launch_owner_counts(c->U, c->bcount, c->owner_counts_p[c->slot], fs);
+    hipMemcpyAsync(c->h_counts + (size_t)c->slot * FR_MAX_SHARD_RANKS, c->owner_counts_p[c->slot],
+                   sizeof(uint32_t) * FR_MAX_SHARD_RANKS, hipMemcpyDeviceToHost, fs);
+    hipEventRecord(c->ev_counts[c->slot], fs);
+  }
   c->compacted = false;
   return check_launch(c);
 }
@@ -930,13 +812,27 @@ int fr_composite_views(fr_ctx* c, const void* views, int nviews, void* out, size
   return FR_OK;
 }
 
-int fr_set_gaze(fr_ctx* c, float x, float y) {
-  // cursorPosCallback (FR/gui.cpp:48-66) sets g_gaze in window coordinates (y down); the kernels
-  // use (g_gaze.x, H - g_gaze.y) (FR/PathTracer.cpp:796-797)
-  if (!c || !std::isfinite(x) || !std::isfinite(y)) return FR_E_INVALID;
-  // off-window cursors are kept as given (the log-polar mask and the gaze distance are defined for
-  // any gaze); the two texel reads at the gaze clamp to the screen (k_sampling, fr_gaze_target)
-  c->U.gaze = mk2(x, (float)c->H - y);
+// g_gaze is a Win32 POINT (LONG x, y; FR/gui.h:14) and the cursor a double: the assignment truncates
+// toward zero (clamped to the LONG range here, where C++ leaves it undefined)
+static long to_long(double v) { return (long)std::max(-2147483648.0, std::min(2147483647.0, std::trunc(v))); }
+static void set_g_gaze(fr_ctx* c, long gx, long gy) {
+  // m_context["gaze"] = (float(g_gaze.x), float(g_screenSize.cy - g_gaze.y)) (FR/PathTracer.cpp:795); off-window
+  // cursors are kept as given (the log-polar mask and the gaze distance are defined for any gaze); the two
+  // texel reads at the gaze clamp to the screen (k_sampling, fr_gaze_target)
+  c->U.gaze = mk2((float)gx, (float)((long)c->H - gy));
+}
+int fr_set_gaze(fr_ctx* c, double xpos, double ypos, int fullscreen) {
+  // cursorPosCallback (FR/gui.cpp:48-66): adjust_scale = g_fullScreen ? 1 : 1.25 (:51-56);
+  // g_gaze.x = xpos; g_gaze.y = ypos * adjust_scale (:65-66, and :59-60 on the first call)
+  if (!c || !std::isfinite(xpos) || !std::isfinite(ypos)) return FR_E_INVALID;
+  const float adjust_scale = fullscreen ? 1.0f : 1.25f;
+  set_g_gaze(c, to_long(xpos), to_long(ypos * adjust_scale));
+  return FR_OK;
+}
+int fr_reset_gaze(fr_ctx* c) {
+  // framebufferSizeCallback (FR/gui.cpp:32-35): g_gaze = (w / 2, h / 2), integer division
+  if (!c) return FR_E_INVALID;
+  set_g_gaze(c, c->W / 2, c->H / 2);
   return FR_OK;
 }
 
@@ -958,6 +854,13 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     // untimed frames pipeline: the front stages go to stream5 and overlap the previous frame's
     // entry 3 (timed frames keep every stage on `stream`, one after the other)
     hipStream_t fs = t ? c->stream : c->stream5;
+    if (!t && c->stream_dirty) {
+      // the front stages overwrite buffers (gclass, DIFFUSE, EXTRA, depth, ballots, counts, lp_cache) that
+      // work enqueued on `stream` by other calls may still read: order them after it explicitly
+      hipEventRecord(c->ev[18], c->stream);
+      hipStreamWaitEvent(fs, c->ev[18], 0);
+    }
+    c->stream_dirty = false;
     if ((rc = enqueue_geometry(c, fs))) return rc;
     if (t) hipEventRecord(ev[1], c->stream);
     if ((rc = enqueue_sampling(c, fs))) return rc;
@@ -983,19 +886,21 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     // half (on `stream`) overlaps it. Two independent chains read the shading: JFA -> Sibson
     // (stream3) and pull-push -> A-Trous (stream2; atFS binds the JFA texture but never reads it,
     // FR/shader/atFS.glsl:40-90). Both resolve their inputs now, at this frame's slot.
+    // (a group's reconstruction rank may run only one of the chains: c->recon_chains)
     hipEventRecord(ev[16], c->stream);
     hipStreamWaitEvent(c->stream3, ev[16], 0);
     hipStreamWaitEvent(c->stream2, ev[16], 0);
     if (t) hipEventRecord(ev[20], c->stream3);
-    if ((rc = enqueue_jfa(c, FR_BUF_SHADING, c->stream3))) return rc;
+    if ((c->recon_chains & 1) && (rc = enqueue_jfa(c, FR_BUF_SHADING, c->stream3))) return rc;
     if (t) hipEventRecord(ev[21], c->stream3);
-    if ((rc = enqueue_sibson(c, c->stream3))) return rc;
+    if ((c->recon_chains & 1) && (rc = enqueue_sibson(c, c->stream3))) return rc;
     if (t) hipEventRecord(ev[22], c->stream3);
+    if (c->recon_gate) hipStreamWaitEvent(c->stream2, c->recon_gate, 0);
     if (t) hipEventRecord(ev[13], c->stream2);
-    if ((rc = enqueue_pullpush(c, FR_BUF_SHADING, c->stream2))) return rc;
+    if ((c->recon_chains & 2) && (rc = enqueue_pullpush(c, FR_BUF_SHADING, c->stream2))) return rc;
     if (t) hipEventRecord(ev[14], c->stream2);
-    if ((rc = enqueue_atrous(c, c->cfg.atrous_iterations, FR_BUF_POSITION, FR_BUF_NORMAL, FR_BUF_PULLPUSH,
-                             c->stream2))) return rc;
+    if ((c->recon_chains & 2) && (rc = enqueue_atrous(c, c->cfg.atrous_iterations, FR_BUF_POSITION, FR_BUF_NORMAL,
+                                                      FR_BUF_PULLPUSH, c->stream2))) return rc;
     if (t) hipEventRecord(ev[15], c->stream2);
     hipEventRecord(ev[17], c->stream2);
     hipStreamWaitEvent(c->stream3, ev[17], 0);
@@ -1026,29 +931,103 @@ int fr_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, true, true
 int fr_trace_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, true, false); }
 int fr_reconstruct_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, false, true); }
 
-int fr_set_shard_ex(fr_ctx* c, int rank, int count, int tile, int first_tracer) {
+int fr_shard_plan(int W, int H, int tile, int count, const float* weights, uint8_t* owner, size_t ntiles) {
+  if (W <= 0 || H <= 0 || tile < 16 || tile % 16 || count < 1 || count > FR_MAX_SHARD_RANKS || !owner)
+    return fail(nullptr, FR_E_INVALID, "fr_shard_plan: need W, H > 0, tile a multiple of 16, 1 <= count <= 64");
+  const size_t nt = (size_t)((W + tile - 1) / tile) * ((H + tile - 1) / tile);
+  if (ntiles != nt) return fail(nullptr, FR_E_INVALID, "fr_shard_plan: ntiles != ceil(W/tile) * ceil(H/tile)");
+  std::vector<double> w(count, 1.0);
+  double sum = count;
+  if (weights) {
+    sum = 0.0;
+    for (int r = 0; r < count; r++) {
+      if (!(weights[r] >= 0.0f) || !std::isfinite(weights[r])) return fail(nullptr, FR_E_INVALID, "fr_shard_plan: bad weight");
+      w[r] = weights[r];
+      sum += w[r];
+    }
+    if (sum <= 0.0) return fail(nullptr, FR_E_INVALID, "fr_shard_plan: all weights are 0");
+  }
+  // smooth weighted round robin (raster order): every step each rank earns its weight, the richest
+  // rank (lowest rank on ties) takes the tile and pays the total
+  std::vector<double> cur(count, 0.0);
+  for (size_t t = 0; t < nt; t++) {
+    int best = -1;
+    for (int r = 0; r < count; r++) {
+      if (w[r] <= 0.0) continue;
+      cur[r] += w[r];
+      if (best < 0 || cur[r] > cur[best]) best = r;
+    }
+    cur[best] -= sum;
+    owner[t] = (uint8_t)best;
+  }
+  return FR_OK;
+}
+
+int fr_set_shard_plan(fr_ctx* c, int rank, int count, int tile, const uint8_t* owner, size_t ntiles) {
   if (!c) return FR_E_INVALID;
-  if (count < 1 || rank < 0 || rank >= count || tile < 8 || tile > 4096)
-    return fail(c, FR_E_INVALID, "fr_set_shard: need 0 <= rank < count and 8 <= tile <= 4096");
-  if (first_tracer < 0 || (count > 1 && first_tracer >= count) || (count == 1 && first_tracer != 0))
-    return fail(c, FR_E_INVALID, "fr_set_shard_ex: need 0 <= first_tracer < count (at least one tracing rank)");
+  if (count < 1 || count > FR_MAX_SHARD_RANKS || rank < 0 || rank >= count || tile < 16 || tile % 16 || tile > 4096)
+    return fail(c, FR_E_INVALID, "fr_set_shard: need 0 <= rank < count <= 64 and tile a multiple of 16 in 16..4096");
+  const int tx = (c->W + tile - 1) / tile, ty = (c->H + tile - 1) / tile;
+  const size_t nt = (size_t)tx * ty;
+  if (count > 1 && (!owner || ntiles != nt))
+    return fail(c, FR_E_INVALID, "fr_set_shard_plan: owner must hold ceil(W/tile) * ceil(H/tile) entries");
+  std::vector<uint32_t> map(nt, 0);
+  std::vector<uint32_t> next(count, 0);
+  if (count > 1)
+    for (size_t t = 0; t < nt; t++) {
+      if (owner[t] >= count) return fail(c, FR_E_INVALID, "fr_set_shard_plan: owner out of range");
+      map[t] = (uint32_t)owner[t] << 24 | next[owner[t]]++;
+    }
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream5));
+  if (c->shard_map) { hipFree(c->shard_map); c->shard_map = nullptr; }
+  c->shard_owner.clear();
+  if (count > 1) {
+    HIP_TRY(c, hipMalloc((void**)&c->shard_map, nt * sizeof(uint32_t)));
+    HIP_TRY(c, hipMemcpy(c->shard_map, map.data(), nt * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->shard_owner.assign(owner, owner + nt);
+  }
   c->U.shard_rank = rank;
   c->U.shard_count = count;
   c->U.shard_tile = tile;
-  c->U.shard_tiles_x = (c->W + tile - 1) / tile;
-  c->U.shard_first = first_tracer;
+  c->U.shard_tiles_x = tx;
+  c->U.shard_map = c->shard_map;
   c->compacted = false;
   return FR_OK;
 }
+
+int fr_set_shard_ex(fr_ctx* c, int rank, int count, int tile, int first_tracer) {
+  if (!c) return FR_E_INVALID;
+  if (first_tracer < 0 || (count > 1 && first_tracer >= count) || (count == 1 && first_tracer != 0))
+    return fail(c, FR_E_INVALID, "fr_set_shard_ex: need 0 <= first_tracer < count (at least one tracing rank)");
+  if (count < 1 || tile < 16 || tile % 16) return fail(c, FR_E_INVALID, "fr_set_shard: need count >= 1 and tile a multiple of 16");
+  const size_t nt = (size_t)((c->W + tile - 1) / tile) * ((c->H + tile - 1) / tile);
+  std::vector<uint8_t> owner(nt);
+  for (size_t t = 0; t < nt; t++) owner[t] = (uint8_t)(first_tracer + t % (size_t)(count - first_tracer));
+  return fr_set_shard_plan(c, rank, count, tile, owner.data(), nt);
+}
 int fr_set_shard(fr_ctx* c, int rank, int count, int tile) { return fr_set_shard_ex(c, rank, count, tile, 0); }
+
+int fr_shard_counts(fr_ctx* c, uint32_t* counts, int n) {
+  if (!c || !counts || n < 1) return FR_E_INVALID;
+  if (c->U.shard_count <= 1) return fail(c, FR_E_STATE, "fr_shard_counts: call fr_set_shard with count > 1 first");
+  HIP_TRY(c, hipEventSynchronize(c->ev_counts[c->slot]));
+  for (int r = 0; r < n; r++) counts[r] = r < c->U.shard_count ? c->h_counts[(size_t)c->slot * FR_MAX_SHARD_RANKS + r] : 0;
+  return FR_OK;
+}
 
 int fr_shard_texels(fr_ctx* c, size_t* texels) {
   if (!c || !texels) return FR_E_INVALID;
   const int T = c->U.shard_count > 1 ? c->U.shard_tile : 0;
   if (!T) { *texels = (size_t)c->W * c->H; return FR_OK; }
-  const size_t tiles = (size_t)c->U.shard_tiles_x * ((c->H + T - 1) / T);
-  const size_t tracers = (size_t)(c->U.shard_count - c->U.shard_first);
-  *texels = (tiles + tracers - 1) / tracers * (size_t)T * T;
+  // the largest tile count of any rank (slabs of every rank have one size)
+  std::vector<size_t> per(c->U.shard_count, 0);
+  for (uint8_t o : c->shard_owner) per[o]++;
+  size_t mx = 0;
+  for (size_t v : per) mx = std::max(mx, v);
+  *texels = std::max<size_t>(mx, 1) * (size_t)T * T;
   return FR_OK;
 }
 
@@ -1077,9 +1056,10 @@ int fr_shard_unpack(fr_ctx* c, int id, int src_rank, const void* slab, size_t by
   return shard_io(c, id, src_rank, const_cast<void*>(slab), bytes, false);
 }
 
-int fr_shard_pack_active(fr_ctx* c, void* slab, uint32_t capacity, uint32_t* count) {
+int fr_shard_pack_active(fr_ctx* c, void* slab, size_t slab_bytes, uint32_t capacity, uint32_t* count) {
   if (!c || !slab || !count) return FR_E_INVALID;
   if (c->U.shard_count <= 1) return fail(c, FR_E_STATE, "fr_shard_*: call fr_set_shard with count > 1 first");
+  if (slab_bytes < (size_t)capacity * 20) return fail(c, FR_E_INVALID, "fr_shard_pack_active: slab smaller than 20 * capacity");
   join_recon(c);
   hipSetDevice(c->cfg.device);
   HIP_TRY(c, hipMemcpyAsync(count, c->ray_count, 4, hipMemcpyDeviceToHost, c->stream));
@@ -1094,14 +1074,16 @@ int fr_shard_pack_active(fr_ctx* c, void* slab, uint32_t capacity, uint32_t* cou
   return FR_OK;
 }
 
-int fr_shard_unpack_active(fr_ctx* c, const void* slab, uint32_t capacity, uint32_t count) {
+int fr_shard_unpack_active(fr_ctx* c, const void* slab, size_t slab_bytes, uint32_t capacity, uint32_t count) {
   if (!c || !slab) return FR_E_INVALID;
   if (count > capacity) return fail(c, FR_E_INVALID, "fr_shard_unpack_active: count above capacity");
+  if (slab_bytes < (size_t)capacity * 20) return fail(c, FR_E_INVALID, "fr_shard_unpack_active: slab smaller than 20 * capacity");
   join_recon(c);
   hipSetDevice(c->cfg.device);
   const f4* vals = (const f4*)slab;
   const uint32_t* idx = (const uint32_t*)((const char*)slab + (size_t)capacity * sizeof(f4));
-  launch_shard_unpack_active(vals, idx, count, c->img[c->hist_cache], c->img[P_shd(c)], c->stream);
+  launch_shard_unpack_active(vals, idx, count, (uint32_t)((size_t)c->W * c->H), c->img[c->hist_cache], c->img[P_shd(c)],
+                             c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1367,6 +1349,14 @@ int fr_reset_stats(fr_ctx* c) {
 }
 
 }  // extern "C"
+
+namespace fri {
+int fail(fr_ctx* c, int code, const std::string& msg) { return ::fail(c, code, msg); }
+int check_launch(fr_ctx* c) { return ::check_launch(c); }
+void join_recon(fr_ctx* c) { ::join_recon(c); }
+int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) { return ::frame_half(c, t, trace, recon); }
+int P_shd(const fr_ctx* c) { return ::P_shd(c); }
+}  // namespace fri
 
 struct fr_scene {
   HostScene scene;

@@ -99,10 +99,11 @@ struct FrameUniforms {
   int32_t spp;
   int32_t sqrt_spp;
   int32_t mask_mode;
-  // screen-tile sharding of one view across ranks (fr_set_shard_ex): tile t = ty * tiles_x + tx is
-  // traced by rank shard_first + t % (shard_count - shard_first); ranks below shard_first (the view's
-  // reconstruction root) trace none; shard_count 1 = the whole screen
-  int32_t shard_rank, shard_count, shard_tile, shard_tiles_x, shard_first;
+  // screen-tile sharding of one view across ranks (fr_set_shard_plan): tile t = ty * tiles_x + tx is
+  // traced by rank shard_map[t] >> 24, and is that rank's (shard_map[t] & 0xFFFFFF)-th tile (its slot
+  // in a packed tile slab); shard_count 1 = the whole screen (shard_map unused)
+  int32_t shard_rank, shard_count, shard_tile, shard_tiles_x;
+  const uint32_t* shard_map;
 };
 
 // XCD-aware block order: blocks b, b+8, b+16, ... share an XCD (and its L2), so hand each of the 8
@@ -114,13 +115,13 @@ FR_DEV uint32_t xcd_tile(uint32_t bx, uint32_t by, uint32_t gx, uint32_t gy) {
   return k * q + (k < r ? k : r) + i;
 }
 
-FR_HD int shard_owner(const FrameUniforms& U, int t) {
-  return U.shard_first + t % (U.shard_count - U.shard_first);
+FR_DEV int shard_owner(const FrameUniforms& U, int t) { return (int)(U.shard_map[t] >> 24); }
+FR_DEV int shard_tile_of(const FrameUniforms& U, int x, int y) {
+  return (y / U.shard_tile) * U.shard_tiles_x + x / U.shard_tile;
 }
-FR_HD bool shard_owns(const FrameUniforms& U, int x, int y) {
+FR_DEV bool shard_owns(const FrameUniforms& U, int x, int y) {
   if (U.shard_count <= 1) return true;
-  const int t = (y / U.shard_tile) * U.shard_tiles_x + x / U.shard_tile;
-  return shard_owner(U, t) == U.shard_rank;
+  return shard_owner(U, shard_tile_of(U, x, y)) == U.shard_rank;
 }
 
 // Ray-segment statistics, accumulated with one atomic per wave.

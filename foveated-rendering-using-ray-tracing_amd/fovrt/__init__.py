@@ -24,6 +24,8 @@ LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "libfovrt.so")
 REPO_ROOT = os.path.dirname(os.path.dirname(_PKG_DIR))
 DEFAULT_ASSET_DIR = os.path.join(REPO_ROOT, "assets")
 
+ABI_VERSION = 2  # FOVRT_ABI_VERSION of include/fovrt.h this mirror is written against
+GROUP_MAX_VIEW_RANKS = 16
 # fr_status
 FR_OK, FR_E_INVALID, FR_E_HIP, FR_E_NOMEM, FR_E_IO, FR_E_STATE, FR_E_UNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
 # scenes / masks
@@ -48,7 +50,8 @@ class FovrtError(RuntimeError):
 
 
 class fr_config(C.Structure):
-    _fields_ = [("width", C.c_int), ("height", C.c_int), ("scene", C.c_int), ("mask_mode", C.c_int),
+    _fields_ = [("abi_version", C.c_int), ("width", C.c_int), ("height", C.c_int), ("scene", C.c_int),
+                ("mask_mode", C.c_int),
                 ("spp", C.c_int), ("diffuse_max_depth", C.c_int), ("refraction_max_depth", C.c_int),
                 ("light_power", C.c_float), ("optimize", C.c_int), ("atrous_iterations", C.c_int),
                 ("write_extra", C.c_int), ("device", C.c_int), ("texture_mode", C.c_int), ("detail", C.c_int),
@@ -88,6 +91,11 @@ class fr_stage_times(C.Structure):
     _fields_ = [("frames", C.c_uint32), ("shading_ms", C.c_double), ("shade_paths_ms", C.c_double)]
 
 
+class fr_group_config(C.Structure):
+    _fields_ = [("views", C.c_int), ("tile", C.c_int), ("split_recon", C.c_int), ("moving_camera", C.c_int),
+                ("composite", C.c_int), ("recon_cost", C.c_float * 2), ("weights", C.c_float * GROUP_MAX_VIEW_RANKS)]
+
+
 class fr_scene_arrays(C.Structure):
     _fields_ = [("num_tris", C.c_int), ("pos", C.POINTER(C.c_float)), ("nrm", C.POINTER(C.c_float)),
                 ("uv", C.POINTER(C.c_float)), ("flags", C.POINTER(C.c_int32)), ("num_materials", C.c_int),
@@ -101,6 +109,7 @@ class fr_scene_arrays(C.Structure):
 _SIGS = {
     "fr_config_default": [C.POINTER(fr_config)],
     "fr_version": [],
+    "fr_abi_version": [],
     "fr_create": [C.POINTER(fr_config), C.POINTER(C.c_void_p)],
     "fr_destroy": [C.c_void_p],
     "fr_last_error": [C.c_void_p],
@@ -125,15 +134,19 @@ _SIGS = {
     "fr_pullpush_render": [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)],
     "fr_atrous_render": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint64)],
     "fr_logpolar_render": [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)],
-    "fr_set_gaze": [C.c_void_p, C.c_float, C.c_float],
+    "fr_set_gaze": [C.c_void_p, C.c_double, C.c_double, C.c_int],
+    "fr_reset_gaze": [C.c_void_p],
     "fr_composite_views": [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_trace_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_reconstruct_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_set_shard": [C.c_void_p, C.c_int, C.c_int, C.c_int],
     "fr_set_shard_ex": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int],
-    "fr_shard_pack_active": [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)],
-    "fr_shard_unpack_active": [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32],
+    "fr_set_shard_plan": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.c_size_t],
+    "fr_shard_plan": [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_uint8), C.c_size_t],
+    "fr_shard_counts": [C.c_void_p, C.POINTER(C.c_uint32), C.c_int],
+    "fr_shard_pack_active": [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.POINTER(C.c_uint32)],
+    "fr_shard_unpack_active": [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32],
     "fr_shard_texels": [C.c_void_p, C.POINTER(C.c_size_t)],
     "fr_shard_pack": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_shard_unpack": [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t],
@@ -152,6 +165,18 @@ _SIGS = {
     "fr_scene_create": [C.POINTER(fr_config), C.POINTER(C.c_void_p)],
     "fr_scene_get_arrays": [C.c_void_p, C.POINTER(fr_scene_arrays)],
     "fr_scene_destroy": [C.c_void_p],
+    "fr_group_config_default": [C.POINTER(fr_group_config)],
+    "fr_rccl_unique_id": [C.c_void_p],
+    "fr_rccl_comm_init": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)],
+    "fr_rccl_comm_destroy": [C.c_void_p],
+    "fr_group_create": [C.POINTER(C.c_void_p), C.c_int, C.c_void_p, C.POINTER(fr_group_config), C.POINTER(C.c_void_p)],
+    "fr_group_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
+    "fr_group_composite": [C.c_void_p, C.c_void_p, C.c_size_t],
+    "fr_group_rank_info": [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                           C.POINTER(C.c_int)],
+    "fr_group_synchronize": [C.c_void_p],
+    "fr_group_destroy": [C.c_void_p],
+    "fr_group_last_error": [],
 }
 
 _lib = None
@@ -170,7 +195,9 @@ def load_library(path: str | None = None):
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = C.c_char_p if name in ("fr_version", "fr_last_error") else C.c_int
+        fn.restype = C.c_char_p if name in ("fr_version", "fr_last_error", "fr_group_last_error") else C.c_int
+    if lib.fr_abi_version() != ABI_VERSION:
+        raise FovrtError(FR_E_STATE, f"{path}: ABI version {lib.fr_abi_version()}, this mirror expects {ABI_VERSION}")
     _lib = lib
     return lib
 
@@ -295,6 +322,8 @@ class Config:
             name = f[0]
             if name == "asset_dir":
                 c.asset_dir = self.asset_dir.encode()
+            elif name == "abi_version":
+                c.abi_version = ABI_VERSION
             else:
                 setattr(c, name, getattr(self, name))
         return c
@@ -475,14 +504,31 @@ class PathTracer:
         n = a.size // 9
         self._check(_lib.fr_set_positions(self._ctx, a.ctypes.data_as(C.POINTER(C.c_float)), n))
 
-    def set_gaze(self, x, y):
-        """cursorPosCallback (FR/gui.cpp:48-66): gaze in window coordinates (y down)."""
-        self._check(_lib.fr_set_gaze(self._ctx, float(x), float(y)))
+    def set_gaze(self, xpos, ypos, fullscreen=False):
+        """cursorPosCallback (FR/gui.cpp:48-66): the cursor in window coordinates (y down);
+        g_gaze = (LONG(xpos), LONG(ypos * adjust_scale)), adjust_scale 1 in full screen, 1.25 in a window."""
+        self._check(_lib.fr_set_gaze(self._ctx, float(xpos), float(ypos), 1 if fullscreen else 0))
+
+    def reset_gaze(self):
+        """framebufferSizeCallback (FR/gui.cpp:32-35): g_gaze = (W / 2, H / 2)."""
+        self._check(_lib.fr_reset_gaze(self._ctx))
 
     # tile sharding of one view across ranks (include/fovrt.h, fr_set_shard)
     def set_shard(self, rank, count, tile=128, first_tracer=0):
         """fr_set_shard_ex: tiles dealt round robin over ranks first_tracer .. count-1."""
         self._check(_lib.fr_set_shard_ex(self._ctx, int(rank), int(count), int(tile), int(first_tracer)))
+
+    def set_shard_plan(self, rank, count, tile, owner):
+        """fr_set_shard_plan: owner[t] (uint8, one per tile in raster order) traces tile t."""
+        o = np.ascontiguousarray(owner, dtype=np.uint8)
+        self._check(_lib.fr_set_shard_plan(self._ctx, int(rank), int(count), int(tile),
+                                           o.ctypes.data_as(C.POINTER(C.c_uint8)), o.size))
+
+    def shard_counts(self, n) -> np.ndarray:
+        """Active pixels of every view rank in the last front stages, from this rank's own full mask."""
+        out = np.zeros(int(n), np.uint32)
+        self._check(_lib.fr_shard_counts(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), int(n)))
+        return out
 
     def shard_texels(self) -> int:
         n = C.c_size_t()
@@ -498,15 +544,17 @@ class PathTracer:
         self._check(_lib.fr_shard_unpack(self._ctx, int(buffer_id), int(src_rank), C.c_void_p(device_ptr),
                                          int(nbytes)))
 
-    def shard_pack_active(self, device_ptr, capacity) -> int:
+    def shard_pack_active(self, device_ptr, capacity, slab_bytes=None) -> int:
         """Packs the pixels this rank's last trace half shaded (capacity x 20 B slab); returns their count."""
         n = C.c_uint32()
-        self._check(_lib.fr_shard_pack_active(self._ctx, C.c_void_p(device_ptr), int(capacity), C.byref(n)))
+        nb = int(capacity) * 20 if slab_bytes is None else int(slab_bytes)
+        self._check(_lib.fr_shard_pack_active(self._ctx, C.c_void_p(device_ptr), nb, int(capacity), C.byref(n)))
         return n.value
 
-    def shard_unpack_active(self, device_ptr, capacity, count):
+    def shard_unpack_active(self, device_ptr, capacity, count, slab_bytes=None):
         """Scatters another rank's packed pixels into HISTORY_CACHE and SHADING."""
-        self._check(_lib.fr_shard_unpack_active(self._ctx, C.c_void_p(device_ptr), int(capacity), int(count)))
+        nb = int(capacity) * 20 if slab_bytes is None else int(slab_bytes)
+        self._check(_lib.fr_shard_unpack_active(self._ctx, C.c_void_p(device_ptr), nb, int(capacity), int(count)))
 
     def synchronize(self):
         self._check(_lib.fr_synchronize(self._ctx))
@@ -630,3 +678,108 @@ class ATrous(_Pass):
 
 def version():
     return load_library().fr_version().decode()
+
+
+def shard_plan(width, height, tile, count, weights=None) -> np.ndarray:
+    """fr_shard_plan (host only): tile owners dealt by smooth weighted round robin in raster order."""
+    lib = load_library()
+    nt = ((width + tile - 1) // tile) * ((height + tile - 1) // tile)
+    owner = np.zeros(nt, np.uint8)
+    w = None if weights is None else (C.c_float * count)(*[float(x) for x in weights])
+    rc = lib.fr_shard_plan(int(width), int(height), int(tile), int(count), w,
+                           owner.ctypes.data_as(C.POINTER(C.c_uint8)), nt)
+    if rc:
+        raise FovrtError(rc, lib.fr_last_error(None).decode())
+    return owner
+
+
+def rccl_unique_id() -> bytes:
+    """fr_rccl_unique_id: the 128-byte RCCL id rank 0 creates and every rank passes to Group.rccl."""
+    lib = load_library()
+    buf = (C.c_uint8 * 128)()
+    rc = lib.fr_rccl_unique_id(buf)
+    if rc:
+        raise FovrtError(rc, lib.fr_group_last_error().decode())
+    return bytes(buf)
+
+
+class Group:
+    """fr_group_*: R ranks (one PathTracer each) rendering `views` views, tile-sharded, with the sparse
+    gather to the reconstruction ranks and the optional composite on rank 0 (include/fovrt.h).
+
+    Group(tracers) puts every rank in this process (device-to-device copies); Group.rccl(tracer, id,
+    nranks, rank) makes this process's tracer one rank of an RCCL communicator."""
+
+    def __init__(self, tracers, views=1, tile=128, split_recon=True, moving_camera=False, composite=False,
+                 recon_cost=None, weights=None, _comm=None):
+        lib = load_library()
+        cfg = fr_group_config()
+        lib.fr_group_config_default(C.byref(cfg))
+        cfg.views, cfg.tile = int(views), int(tile)
+        cfg.split_recon, cfg.moving_camera, cfg.composite = int(bool(split_recon)), int(bool(moving_camera)), int(bool(composite))
+        if recon_cost is not None:
+            cfg.recon_cost[0], cfg.recon_cost[1] = float(recon_cost[0]), float(recon_cost[1])
+        if weights is not None:
+            for i, w in enumerate(weights):
+                cfg.weights[i] = float(w)
+        self.tracers = list(tracers)
+        arr = (C.c_void_p * len(self.tracers))(*[t._ctx.value for t in self.tracers])
+        h = C.c_void_p()
+        rc = lib.fr_group_create(arr, len(self.tracers), _comm, C.byref(cfg), C.byref(h))
+        if rc:
+            raise FovrtError(rc, lib.fr_group_last_error().decode())
+        self._h = h
+        self._comm = _comm
+        self._owns_comm = False
+        self.config = cfg
+
+    @classmethod
+    def rccl(cls, tracer, unique_id: bytes, nranks, rank, **kw):
+        lib = load_library()
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        comm = C.c_void_p()
+        rc = lib.fr_rccl_comm_init(buf, int(nranks), int(rank), int(tracer.config.device), C.byref(comm))
+        if rc:
+            raise FovrtError(rc, lib.fr_group_last_error().decode())
+        try:
+            g = cls([tracer], _comm=comm, **kw)
+        except Exception:
+            lib.fr_rccl_comm_destroy(comm)
+            raise
+        g._owns_comm = True
+        return g
+
+    def _check(self, rc):
+        if rc:
+            raise FovrtError(rc, _lib.fr_group_last_error().decode())
+
+    def frame(self, timing=False):
+        """One frame of every local rank; timing=True returns one stage-time dict per local rank."""
+        if not timing:
+            self._check(_lib.fr_group_frame(self._h, None))
+            return None
+        t = (fr_frame_timing * len(self.tracers))()
+        self._check(_lib.fr_group_frame(self._h, t))
+        return [{n: getattr(x, n) for n, _ in fr_frame_timing._fields_} for x in t]
+
+    def composite(self, device_ptr, nbytes):
+        self._check(_lib.fr_group_composite(self._h, C.c_void_p(device_ptr), int(nbytes)))
+
+    def rank_info(self, i):
+        v, vr, ch, tl = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        self._check(_lib.fr_group_rank_info(self._h, int(i), C.byref(v), C.byref(vr), C.byref(ch), C.byref(tl)))
+        return {"view": v.value, "view_rank": vr.value, "chains": ch.value, "tiles": tl.value}
+
+    def synchronize(self):
+        self._check(_lib.fr_group_synchronize(self._h))
+
+    def destroy(self):
+        if getattr(self, "_h", None) is not None and _lib is not None:
+            _lib.fr_group_destroy(self._h)
+            self._h = None
+            if self._owns_comm and self._comm is not None:
+                _lib.fr_rccl_comm_destroy(self._comm)
+                self._comm = None
+
+    def __del__(self):
+        self.destroy()

@@ -23,7 +23,9 @@
 extern "C" {
 #endif
 
-#define FOVRT_ABI_VERSION 1
+/* 2: fr_config.abi_version; fr_set_gaze takes the cursor (cursorPosCallback) and fr_reset_gaze; the
+ *    sparse shard calls take the slab size; fr_set_shard_plan / fr_shard_plan; the fr_group_* calls. */
+#define FOVRT_ABI_VERSION 2
 
 typedef enum fr_status {
   FR_OK = 0,
@@ -52,6 +54,7 @@ typedef enum fr_mask_mode {
 } fr_mask_mode;
 
 typedef struct fr_config {
+  int abi_version;            /* FOVRT_ABI_VERSION (fr_config_default sets it; fr_create rejects others) */
   int width, height;          /* FR/main.cpp:127-135 (argv W H), default 1024 x 1024 */
   int scene;                  /* fr_scene_preset */
   int mask_mode;              /* fr_mask_mode */
@@ -160,6 +163,7 @@ typedef struct fr_ctx fr_ctx;
 
 int fr_config_default(fr_config* cfg);
 const char* fr_version(void);
+int fr_abi_version(void);  /* FOVRT_ABI_VERSION of the library */
 
 /* PathTracer::initialize(w, h) (FR/PathTracer.cpp:41-78) + the renderer constructors
  * (FR/main.cpp:152-159). */
@@ -203,9 +207,14 @@ int fr_logpolar_render(fr_ctx* ctx, int in_buffer, uint64_t* elapsed_ns);
  * device `views` = nviews consecutive W x H RGBA32F images -> device `out` = (nviews * W) x H,
  * view v in columns [v W, (v+1) W) (renderAll's side-by-side display, FR/main.cpp:26-113). */
 int fr_composite_views(fr_ctx* ctx, const void* views, int nviews, void* out, size_t out_bytes);
-/* Gaze input (cursorPosCallback, FR/gui.cpp:48-66): window coordinates, y down; the kernels use
- * (x, H - y) from the next launch on (also replaced by fr_set_camera's gaze). */
-int fr_set_gaze(fr_ctx* ctx, float x, float y);
+/* Gaze input, the reference's GLFW callbacks. fr_set_gaze is cursorPosCallback (FR/gui.cpp:48-66): the
+ * cursor (xpos, ypos) in window coordinates (y down) sets the Win32 POINT g_gaze = ((LONG)xpos,
+ * (LONG)(ypos * adjust_scale)), adjust_scale = 1 in full screen (g_fullScreen) and 1.25 in a window
+ * (:51-56); fr_reset_gaze is framebufferSizeCallback's g_gaze = (w / 2, h / 2) (:32-35). The kernels use
+ * (g_gaze.x, H - g_gaze.y) (FR/PathTracer.cpp:795) from the next launch on; fr_set_camera's gaze
+ * replaces it too. */
+int fr_set_gaze(fr_ctx* ctx, double xpos, double ypos, int fullscreen);
+int fr_reset_gaze(fr_ctx* ctx);
 
 /* The whole main.cpp loop body (update -> 0 -> 1 -> 2 -> 3 -> JFA -> SI -> PPI -> AT). With timing == NULL
  * nothing is synchronised and consecutive frames pipeline: frame N's reconstruction (JFA -> Sibson and
@@ -226,25 +235,91 @@ int fr_synchronize(fr_ctx* ctx);
  * tiles of SHADING and runs the reconstruction half. Exact for a static camera (history is
  * per-tile); with a moving camera also exchange HISTORY_CACHE the same way. count = 1 restores the
  * whole screen. Slabs are device buffers of fr_shard_texels() RGBA32F texels (T*T per owned tile,
- * owned tiles in increasing order); pack/unpack synchronise the context stream. */
+ * owned tiles in increasing order); pack/unpack synchronise the context stream. (fr_group_* below
+ * runs all of this, RCCL included, behind one call per frame.) */
 int fr_set_shard(fr_ctx* ctx, int rank, int count, int tile);
+/* Explicit tile owners: owner[t] (< count) traces tile t (ntiles = ceil(W/tile) * ceil(H/tile)). */
+int fr_set_shard_plan(fr_ctx* ctx, int rank, int count, int tile, const uint8_t* owner, size_t ntiles);
+/* Host only (no device): deals the ntiles tiles of a W x H screen over count ranks in proportion to
+ * weights[0..count-1] (>= 0, not all 0) by smooth weighted round robin in raster order, so every rank
+ * gets its share of the dense foveal tiles. weights NULL = equal. Writes owner[0..ntiles-1]. */
+int fr_shard_plan(int width, int height, int tile, int count, const float* weights, uint8_t* owner, size_t ntiles);
+/* Active pixels of every rank of the view in the last front stages (sampling + compaction), counted
+ * on this rank from its own full mask: the pixels rank r traces and sends. Synchronises the front. */
+int fr_shard_counts(fr_ctx* ctx, uint32_t* counts, int n);
 /* The same with the tiles dealt over ranks first_tracer .. count-1 only (tile t to rank
  * first_tracer + t % (count - first_tracer)); ranks below first_tracer trace nothing. first_tracer = 1
  * leaves the view's compositing rank 0 to the G-buffer and the reconstruction half, which no other
  * rank can share (JFA's reach, the global pull-push pyramid). fr_set_shard = first_tracer 0. */
 int fr_set_shard_ex(fr_ctx* ctx, int rank, int count, int tile, int first_tracer);
-/* Sparse SHADING gather for a static camera (SURVEY §8(e) "sparse variant"): a tracing rank packs only
- * the pixels its last trace half shaded, as capacity x 16 B of history texels followed by capacity x 4 B
- * of pixel indices (slab >= 20 x capacity bytes); *count returns their number (FR_E_INVALID when it
- * exceeds capacity: size capacity from fr_ray_count). The compositing rank, after its own trace half
- * (which carries every other pixel's history), scatters each rank's entries into HISTORY_CACHE and
- * SHADING. ~10x less than the tile slabs at a 10 % mask. With a moving camera use the tile slabs and
- * the HISTORY_CACHE exchange. Both synchronise the context stream. */
-int fr_shard_pack_active(fr_ctx* ctx, void* device_slab, uint32_t capacity, uint32_t* count);
-int fr_shard_unpack_active(fr_ctx* ctx, const void* device_slab, uint32_t capacity, uint32_t count);
+/* Sparse SHADING gather (SURVEY §8(e) "sparse variant"): a tracing rank packs only the pixels its last
+ * trace half shaded, as capacity x 16 B of history texels followed by capacity x 4 B of pixel indices
+ * (slab_bytes >= 20 x capacity, else FR_E_INVALID); *count returns their number (FR_E_INVALID when it
+ * exceeds capacity: size capacity from fr_ray_count). A receiving rank, after its own trace half (which
+ * carries every other pixel's history), scatters each rank's entries into HISTORY_CACHE and SHADING
+ * (indices outside the screen are skipped). ~10x less than the tile slabs at a 10 % mask. Exact for a
+ * static camera when the compositing rank receives; with a moving camera when every rank receives
+ * every other rank's pixels each frame (its reprojection then reads a complete history). Both
+ * synchronise the context stream. */
+int fr_shard_pack_active(fr_ctx* ctx, void* device_slab, size_t slab_bytes, uint32_t capacity, uint32_t* count);
+int fr_shard_unpack_active(fr_ctx* ctx, const void* device_slab, size_t slab_bytes, uint32_t capacity,
+                           uint32_t count);
 int fr_shard_texels(fr_ctx* ctx, size_t* texels);
 int fr_shard_pack(fr_ctx* ctx, int buffer_id, void* device_slab, size_t bytes);
 int fr_shard_unpack(fr_ctx* ctx, int buffer_id, int src_rank, const void* device_slab, size_t bytes);
+
+/* ---- Multi-GPU groups (SURVEY §8(b) Threading, §8(e)) --------------------------------------------
+ * The reference is single-GPU; this is how frames shard over the GPUs of a node. A group is R ranks
+ * (one fr_ctx each, all created with the same fr_config apart from .device) rendering V views (eyes) of
+ * G = R / V ranks: rank r renders view r / G as view rank r % G (view v's camera is set on its ranks'
+ * contexts with fr_set_camera as usual). In a view the screen tiles are dealt over the ranks by weight
+ * (fr_shard_plan). Every rank runs the front stages (G-buffer, sampling mask, compaction) and traces its
+ * own tiles' active pixels; each traced pixel (20 B: history texel + pixel index) goes to the view's
+ * reconstruction ranks, which run JumpFlooding -> Sibson (view rank 0) and pull-push -> A-Trous (view
+ * rank 1 with split_recon, else rank 0 as well); the composite is bit-identical to the one-GPU frame.
+ * That gather is the path's only exchange (JFA's reach and the pull-push pyramid are global); it uses
+ * RCCL ncclSend/ncclRecv over xGMI, sized on every rank from its own full mask (fr_shard_counts), so
+ * there is no control collective and no host synchronisation beyond each rank's own front stages. With
+ * moving_camera every rank receives every other rank's pixels instead (reprojection reads across
+ * tiles). The optional composite gathers each view's A-Trous image to rank 0 (the stereo pair of
+ * BASELINE configs[4], side by side, renderAll FR/main.cpp:26-113).
+ * Ranks live either in one process (ctxs[0..n-1], any devices, rccl_comm NULL: device-to-device
+ * copies; n = R) or one per process (n = 1, rccl_comm = an ncclComm_t of R ranks whose rank is this
+ * context's: fr_rccl_comm_init, or the caller's own). */
+#define FR_GROUP_MAX_VIEW_RANKS 16
+typedef struct fr_group fr_group;
+typedef struct fr_group_config {
+  int views;               /* V >= 1, divides R */
+  int tile;                /* screen tile edge, a multiple of 16 (default 128) */
+  int split_recon;         /* 1 (default): the two reconstruction chains on view ranks 0 and 1 when G >= 2 */
+  int moving_camera;       /* 1: every rank receives every other rank's traced pixels (default 0) */
+  int composite;           /* 1: every frame, the views' A-Trous images side by side on rank 0 */
+  float recon_cost[2];     /* the reconstruction work of view ranks 0 and 1 as a fraction of one frame's
+                              trace work (default 0.5, 0.17: JFA + Sibson, pull-push + A-Trous at 4K);
+                              the tiles are dealt so that every rank's total is level (water filling) */
+  float weights[FR_GROUP_MAX_VIEW_RANKS];  /* explicit tracing weights per view rank; all 0 = from recon_cost */
+} fr_group_config;
+int fr_group_config_default(fr_group_config* cfg);
+/* RCCL bootstrap for callers without their own: rank 0 creates the 128-byte unique id, every rank
+ * passes it (sent by any means) to fr_rccl_comm_init on its own device. */
+int fr_rccl_unique_id(void* id128);
+int fr_rccl_comm_init(const void* id128, int nranks, int rank, int device, void** comm);
+int fr_rccl_comm_destroy(void* comm);
+int fr_group_create(fr_ctx* const* ctxs, int n, void* rccl_comm, const fr_group_config* cfg, fr_group** out);
+/* One frame of every local rank (update -> 0 -> 1 -> 2 -> 3, exchange, JFA -> SI and PPI -> AT on the
+ * reconstruction ranks, the composite). timing == NULL: nothing is synchronised beyond the front stages'
+ * counts, and consecutive frames pipeline. timing != NULL (n timings, one per local rank): the frame is
+ * synchronised and each rank's stage times are returned (reconstruction stages 0 on other ranks). */
+int fr_group_frame(fr_group* g, fr_frame_timing* timing);
+/* Final composite (the group must have composite = 1): copies the last frame's (V * W) x H RGBA32F image
+ * from rank 0 to device memory `out` of rank 0's device (bytes >= V * W * H * 16); synchronises. */
+int fr_group_composite(fr_group* g, void* out, size_t bytes);
+/* Roles of local rank i: *view, *view_rank, *chains (bit 0 JFA -> Sibson, bit 1 pull-push -> A-Trous
+ * run here) and *tiles, the number of screen tiles it traces. */
+int fr_group_rank_info(fr_group* g, int i, int* view, int* view_rank, int* chains, int* tiles);
+int fr_group_synchronize(fr_group* g);
+int fr_group_destroy(fr_group* g);  /* the contexts trace the whole screen again */
+const char* fr_group_last_error(void);  /* the failure of the calling thread's last fr_group_* / fr_rccl_* call */
 
 
 /* GPU BVH builder (the reference's OptiX acceleration rebuild,

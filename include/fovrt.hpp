@@ -124,7 +124,7 @@ class PathTracer {
  public:
   enum TextureName { POSITION, NORMAL, DEPTH, DIFFUSE, WEIGHT, THREAD, HISTORY, SHADING, EXTRA };
 
-  PathTracer() { fr_config_default(&cfg_); }
+  PathTracer() { fr_config_default(&cfg_); }  // cfg.abi_version = FOVRT_ABI_VERSION
   explicit PathTracer(const fr_config& cfg) : cfg_(cfg) {}
   PathTracer(const PathTracer&) = delete;
   PathTracer& operator=(const PathTracer&) = delete;
@@ -162,9 +162,12 @@ class PathTracer {
   void set_positions(const float* xyz, size_t ntris) {  // moved vertices + GPU rebuild (fr_set_positions)
     check(fr_set_positions(ctx(), xyz, ntris), ctx_, "set_positions");
   }
-  void set_gaze(float x, float y) {  // cursorPosCallback (FR/gui.cpp:48-66): window coordinates, y down
-    check(fr_set_gaze(ctx(), x, y), ctx_, "set_gaze");
+  // cursorPosCallback (FR/gui.cpp:48-66): the cursor in window coordinates (y down); adjust_scale 1.25
+  // in a window, 1 in full screen (g_fullScreen)
+  void set_gaze(double xpos, double ypos, bool fullscreen = false) {
+    check(fr_set_gaze(ctx(), xpos, ypos, fullscreen ? 1 : 0), ctx_, "set_gaze");
   }
+  void reset_gaze() { check(fr_reset_gaze(ctx()), ctx_, "reset_gaze"); }  // framebufferSizeCallback (:32-35)
   unsigned int ray_count() {  // m_context["ray_count"] (FR/main.cpp:288-299)
     uint32_t n = 0;
     check(fr_ray_count(ctx(), &n), ctx_, "ray_count");
@@ -204,6 +207,29 @@ inline void finish(uint64_t ns, uint64_t* elapsed, int* done) {
   if (done) *done = 1;
 }
 }  // namespace detail
+
+// GBuffer (FR/GBuffer.h:27-64): the reference constructs it and calls render() every frame
+// (FR/main.cpp:153,255), but its constructor never builds the FBO, VAO or shader (FR/GBuffer.cpp:11-26)
+// and nothing reads its textures; the G-buffer that feeds the path is OptiX entry 0
+// (PathTracer::geometry_launch). The facade keeps those lines compiling: render() does no work and
+// reports 0 ns, and the texture names are the "no texture" 0 of an unbuilt FBO.
+class GBuffer {
+ public:
+  GBuffer() = default;
+  void render(const unsigned* /*query*/ = nullptr, uint64_t* elapsed_time = nullptr, int* done = nullptr) {
+    detail::finish(0, elapsed_time, done);
+  }
+  void BindBuffers() {}
+  void resetFrameCount() {}
+  void resetShader() {}
+  void genScene() {}
+  void loadMesh(const char*) {}
+  void setupMesh() {}
+  const Texture positionTex{};
+  const Texture normalTex{};
+  const Texture depthTex{};
+  const unsigned fbo = 0;
+};
 
 class JumpFlooding {
  public:
@@ -285,6 +311,34 @@ class ATrous {
 
  private:
   PathTracer& t_;
+};
+
+// Multi-GPU group (fr_group_*): one object per process; ranks = the local tracers (in-process copies)
+// or this process's tracer in an RCCL communicator.
+class Group {
+ public:
+  Group(std::vector<PathTracer*> tracers, void* rccl_comm, const fr_group_config& cfg) {
+    std::vector<fr_ctx*> c;
+    for (PathTracer* t : tracers) c.push_back(t->ctx());
+    check(fr_group_create(c.data(), (int)c.size(), rccl_comm, &cfg, &g_), nullptr, "fr_group_create");
+    n_ = (int)c.size();
+  }
+  Group(const Group&) = delete;
+  Group& operator=(const Group&) = delete;
+  ~Group() { if (g_) fr_group_destroy(g_); }
+  void frame() { check(fr_group_frame(g_, nullptr), nullptr, "fr_group_frame"); }
+  std::vector<fr_frame_timing> frame_timed() {
+    std::vector<fr_frame_timing> t((size_t)n_);
+    check(fr_group_frame(g_, t.data()), nullptr, "fr_group_frame");
+    return t;
+  }
+  void composite(void* device_out, size_t bytes) { check(fr_group_composite(g_, device_out, bytes), nullptr, "fr_group_composite"); }
+  void synchronize() { check(fr_group_synchronize(g_), nullptr, "fr_group_synchronize"); }
+  fr_group* handle() const { return g_; }
+
+ private:
+  fr_group* g_ = nullptr;
+  int n_ = 0;
 };
 
 }  // namespace fovrt

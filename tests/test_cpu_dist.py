@@ -1,5 +1,6 @@
-"""World-size-2 gloo rehearsal of bench.py's multi-GPU path (one process per GPU, weak scaling over
-views): per-rank view offsets and the max-time / sum-of-rays reduction over ranks."""
+"""gloo rehearsal of bench.py's multi-GPU path on CPU (one process per GPU): per-rank view offsets, the
+max-time / sum-of-rays reduction over ranks, the RCCL-id bootstrap of libfovrt's group, and the host-side
+tile plan of fr_group (fr_shard_plan; no device needed)."""
 import os
 import socket
 
@@ -52,45 +53,41 @@ def test_single_process_passthrough():
     assert np.allclose(bench.view_offset(0, 1), 0)
 
 
-def _tile_worker(rank, world, views, port, q):
-    import torch
+def _id_worker(rank, world, port, q):
     import torch.distributed as dist
     import bench
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    view, vrank, g = bench.view_layout(rank, world, views)
-    groups = bench.make_view_groups(dist, world, views)
-    slab = torch.full((8,), float(rank))
-    gl = [torch.empty_like(slab) for _ in range(g)] if vrank == 0 else None
-    bench.gather_slabs(dist, groups[view], slab, gl, view * g)
-    al = [torch.empty_like(slab) for _ in range(g)]  # the moving-camera history exchange
-    bench.allgather_slabs(dist, groups[view], slab, al)
-    q.put((rank, view, vrank, g, None if gl is None else [float(t[0]) for t in gl], [float(t[0]) for t in al]))
+    # rank 0's RCCL unique id (fr_rccl_unique_id needs a device; any 128 bytes stand in for it here)
+    uid = bench.broadcast_id(dist, rank, lambda: bytes(range(100, 228)))
+    view, vrank, g = bench.view_layout(rank, world, 2)
+    q.put((rank, uid, view, vrank, g))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_tile_gather_groups_gloo_world4():
-    """4 ranks, 2 views (the stereo layout of BASELINE configs[4] at half size): each view's 2 ranks
-    gather their slabs to the view's first rank, and all-gather them within the view."""
+def test_rccl_id_bootstrap_gloo_world4():
+    """bench.py's bootstrap of libfovrt's RCCL group: rank 0's 128-byte id reaches every rank over gloo;
+    4 ranks in 2 views (the stereo layout of BASELINE configs[4] at half size)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_tile_worker, args=(r, 4, 2, port, q)) for r in range(4)]
+    procs = [ctx.Process(target=_id_worker, args=(r, 4, port, q)) for r in range(4)]
     for p in procs:
         p.start()
     out = {r: rest for r, *rest in (q.get(timeout=120) for _ in procs)}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert out[0][:4] == [0, 0, 2, [0.0, 1.0]] and out[2][:4] == [1, 0, 2, [2.0, 3.0]]
-    assert out[1][3] is None and out[3][3] is None
-    assert out[0][4] == out[1][4] == [0.0, 1.0] and out[2][4] == out[3][4] == [2.0, 3.0]
+    for r in range(4):
+        assert out[r][0] == bytes(range(100, 228))
+        assert tuple(out[r][1:]) == (r // 2, r % 2, 2)
 
 
 def test_view_layout():
     import bench
-    assert bench.view_layout(5, 8, 0) == (5, 0, 1)   # default: one view per rank
+    assert bench.view_layout(5, 8, 0) == (0, 5, 8)   # default: one view tiled over every rank
+    assert bench.view_layout(5, 8, 8) == (5, 0, 1)   # one view per rank
     assert bench.view_layout(5, 8, 2) == (1, 1, 4)   # stereo, 4-way tiles per eye
     assert bench.view_layout(3, 4, 1) == (0, 3, 4)   # one view tiled over 4 ranks
     with pytest.raises(SystemExit):
@@ -108,3 +105,29 @@ def test_view_segments_count_the_gbuffer_once_per_view():
     ranks = [{"segments": W * H + 10 * r, "gbuffer_primary": W * H} for r in range(G)]
     total = sum(bench.view_segments(s, G, r)[0] for r, s in enumerate(ranks))
     assert total == W * H + sum(10 * r for r in range(G))
+
+
+def test_shard_plan_deals_tiles_by_weight():
+    """fr_shard_plan (host only): smooth weighted round robin in raster order. Tile counts follow the
+    weights to within one tile, zero-weight ranks get none, and equal weights give plain round robin."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)),
+                                    "foveated-rendering-using-ray-tracing_amd"))
+    import fovrt
+    W, H, T = 3840, 2160, 128
+    nt = 30 * 17
+    eq = fovrt.shard_plan(W, H, T, 4)
+    assert eq.shape == (nt,) and np.array_equal(eq, np.arange(nt) % 4)
+    w = [0.0, 0.4, 1.0, 1.0]
+    p = fovrt.shard_plan(W, H, T, 4, w)
+    counts = np.bincount(p, minlength=4)
+    assert counts[0] == 0 and counts.sum() == nt
+    assert np.all(np.abs(counts - nt * np.array(w) / sum(w)) <= 1.0)
+    # the foveal centre (the tiles around the gaze) is shared by every weighted rank
+    ty, tx = np.divmod(np.arange(nt), 30)
+    centre = (np.abs(tx - 15) <= 3) & (np.abs(ty - 8) <= 3)
+    assert set(np.unique(p[centre]).tolist()) == {1, 2, 3}
+    with pytest.raises(fovrt.FovrtError):
+        fovrt.shard_plan(W, H, 8, 4)  # tiles are multiples of 16
+    with pytest.raises(fovrt.FovrtError):
+        fovrt.shard_plan(W, H, T, 2, [0.0, 0.0])

@@ -194,3 +194,70 @@ def test_atrous_oracle_matches_numpy_restatement(oracle, W, H, count):
     got = oracle.atrous(count, pos, nrm, col)
     ref = atrous_np(count, pos, nrm, col)
     assert np.abs(got - ref).max() <= 2e-6, np.abs(got - ref).max()
+
+
+# ---------------------------------------------------------------------------------------------
+# Second restatements (numpy float32, written from the reference text) of the stages only the oracle
+# pinned before: sampling_step's saliency + masked_sampling, and Sibson. Bit-for-bit agreement.
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("scene,W,H,mask_mode,gaze_shift", [(1, 64, 64, 0, (0, 0)), (2, 96, 64, 0, (0, 0)),
+                                                            (2, 128, 128, 0, (30, -20)), (1, 100, 70, 0, (-60, 25)),
+                                                            (0, 64, 48, 0, (0, 0)), (2, 96, 64, 4, (5, 5)),
+                                                            (1, 64, 64, 2, (0, 0))])
+def test_sampling_matches_numpy_restatement(oracle, fovrt_mod, scene, W, H, mask_mode, gaze_shift):
+    """oracle.sampling (the C++ restatement) against helpers.sampling_np (numpy, from samplingStep.cu and
+    shared_helper_funcs.h) on the oracle's own G-buffer of two frames (the second has a depth cache, so
+    the reprojection-validity path runs), with the reprojection uv perturbed on some pixels (velocity,
+    off-screen and negative uv) and the gaze moved off centre: mask, weight and heat map bit-identical."""
+    from helpers import sampling_np
+    arrays = fovrt_mod.Scene(fovrt_mod.Config(scene=scene, texture_mode=1, detail=1)).arrays()
+    osc = oracle.OracleScene(arrays)
+    cam = fovrt_mod.Camera.preset(scene, W, H)
+    uni = cam.uniforms(W, H)
+    uni.gaze[0] += np.float32(gaze_shift[0])
+    uni.gaze[1] += np.float32(gaze_shift[1])
+    rng = np.random.default_rng(W + H + scene)
+    g0 = oracle.gbuffer(osc, uni, W, H, 0)
+    g1 = oracle.gbuffer(osc, uni, W, H, 1)
+    weight = g1["weight"].copy()
+    pick = rng.random((H, W)) < 0.2
+    weight[pick, 0] += rng.normal(scale=3.0, size=pick.sum()).astype(np.float32)
+    weight[pick, 1] += rng.normal(scale=3.0, size=pick.sum()).astype(np.float32)
+    neg = rng.random((H, W)) < 0.03
+    weight[neg, :2] = -1.0
+    n_valid_total = 0
+    for frame, g, dc in ((0, g0, np.zeros_like(g0["depth"])), (1, g1, g0["depth"])):
+        w_in = weight if frame == 1 else g["weight"]
+        ref = oracle.sampling(osc, uni, W, H, mask_mode, g["position"], g["depth"], dc, w_in, g["normal"],
+                              g["diffuse"])
+        prev_eye = np.array(uni.prev_eye[:], np.float32)
+        m, w, e = sampling_np(W, H, mask_mode, (uni.gaze[0], uni.gaze[1]), prev_eye, arrays["bbox"], g["position"],
+                              g["depth"], dc, w_in, g["normal"], g["diffuse"])
+        assert np.array_equal(m, ref["mask"]), (frame, np.argwhere(m != ref["mask"])[:5])
+        assert equal_nan(w, ref["weight"]), frame
+        assert equal_nan(e, ref["extra"]), (frame, np.argwhere(~np.isclose(e, ref["extra"], rtol=0, atol=0,
+                                                                             equal_nan=True))[:5])
+        n_valid_total += int((w[..., 2] == 1).sum())
+    assert n_valid_total > 0  # the cache-hit path ran
+    if mask_mode == 0:
+        assert 0 < ref["mask"].mean() < 1
+
+
+@pytest.mark.parametrize("W,H,density", [(64, 64, 0.1), (96, 64, 0.03), (128, 128, 0.1), (40, 33, 0.5),
+                                         (64, 48, "single")])
+def test_sibson_matches_numpy_restatement(oracle, W, H, density):
+    """oracle.sibson against helpers.sibson_np (numpy, from sibsonFS.glsl:16-49) on the oracle's JFA
+    output of sparse images: bit-identical, including pixels whose disc wraps past the border (REPEAT)
+    and seed pixels (radius 0: the seed colour itself)."""
+    from helpers import sibson_np
+    rng = np.random.default_rng(W * 7 + H)
+    if density == "single":
+        m = np.zeros((H, W), np.uint8)
+        m[H // 3, W - 1] = 1
+    else:
+        m = (rng.random((H, W)) < density).astype(np.uint8)
+    img = sparse_image(W, H, m, seed=W)
+    coord, color = oracle.jfa(img)
+    ref = oracle.sibson(coord, color)
+    got = sibson_np(coord, color)
+    assert equal_nan(got, ref), np.argwhere(~np.isclose(got, ref, rtol=0, atol=0, equal_nan=True))[:5]

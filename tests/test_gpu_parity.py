@@ -31,6 +31,15 @@ def make_tracer(fovrt, W, H, scene=1, mask=1, spp=1, dmd=1, refr=16, **kw):
     return t
 
 
+def ref_gaze(H, xpos, ypos, fullscreen=False):
+    """The gaze the kernels see after cursorPosCallback (FR/gui.cpp:48-66): g_gaze = (LONG(xpos),
+    LONG(ypos * adjust_scale)) with adjust_scale 1.25 in a window, 1 in full screen, then
+    (g_gaze.x, H - g_gaze.y) (FR/PathTracer.cpp:795)."""
+    gx = int(np.trunc(xpos))
+    gy = int(np.trunc(ypos * (1.0 if fullscreen else 1.25)))
+    return np.float32(gx), np.float32(H - gy)
+
+
 def mismatch_report(a, b):
     bad = ~np.isclose(a, b, rtol=0, atol=0, equal_nan=True)
     if not bad.any():
@@ -76,8 +85,7 @@ def test_sampling_and_compaction_bit_exact(fovrt_mod, oracle, scene, mask_mode, 
     t.set_camera_uniforms(uni)
     if gaze_window is not None:
         t.set_gaze(*gaze_window)
-        uni.gaze[0] = np.float32(gaze_window[0])
-        uni.gaze[1] = np.float32(H) - np.float32(gaze_window[1])
+        uni.gaze[0], uni.gaze[1] = ref_gaze(H, *gaze_window)
     osc = oracle.OracleScene(t.scene_arrays())
     for frame in range(2):  # frame 1 has a valid depth cache -> isValid / reprojection paths
         t.geometry_launch()
@@ -569,7 +577,7 @@ def test_tile_shards_moving_camera_with_history_exchange(fovrt_mod, scene, mask)
     rank all-gathers HISTORY_CACHE after its trace half (bench.py exchange_history). With that exchange
     the composite equals the single-context frame bit for bit; without it, it does not."""
     import torch
-    W, H, nranks, tile = 160, 112, 2, 8
+    W, H, nranks, tile = 160, 112, 2, 16
     mk = lambda: make_tracer(fovrt_mod, W, H, scene=scene, mask=mask, spp=2, dmd=2)
     full, ranks, stale = mk(), [mk() for _ in range(nranks)], [mk() for _ in range(nranks)]
     for group in (ranks, stale):
@@ -633,11 +641,30 @@ def test_logpolar_transform_bit_exact(fovrt_mod, oracle, W, H):
             gaze = (W // 2, H - H // 2)  # the default gaze (FR/gui.cpp:34-35, kernels use H - y)
         else:
             t.set_gaze(*gaze_window)
-            gaze = (np.float32(gaze_window[0]), np.float32(H) - np.float32(gaze_window[1]))
+            gaze = ref_gaze(H, *gaze_window)
         lp.render(TN.SHADING)
         fwd, inv = oracle.logpolar(img, gaze, fwd, inv)  # outputs persist across calls, as GL textures do
         assert equal_nan(t.read(TN.LOGPOLAR), fwd), k
         assert equal_nan(t.read(TN.LOGPOLAR_INVERSE), inv), k
+
+
+def test_set_gaze_follows_the_cursor_mapping(fovrt_mod):
+    """fr_set_gaze = cursorPosCallback: windowed cursors are scaled by adjust_scale = 1.25 in y and
+    truncated to the Win32 POINT; full screen uses 1; fr_reset_gaze = framebufferSizeCallback's
+    (W / 2, H / 2). Checked through the gaze the log-polar mask is built around."""
+    W, H = 160, 96
+    t = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=1, dmd=1)
+    cases = [((40.7, 30.9), False), ((40.7, 30.9), True), ((-3.5, 70.2), False), ((159.9, 0.0), False)]
+    for (x, y), fs in cases:
+        t.set_gaze(x, y, fullscreen=fs)
+        t.frame(timing=False)
+        g = ref_gaze(H, x, y, fs)
+        assert np.array_equal(t.read(TN.MASK), logpolar_mask_np(W, H, g[0], g[1], signed=True)), (x, y, fs)
+    # windowed 30.9 * 1.25 = 38.625 -> 38, full screen 30 : the two masks differ
+    assert ref_gaze(H, 40.7, 30.9)[1] == H - 38 and ref_gaze(H, 40.7, 30.9, True)[1] == H - 30
+    t.reset_gaze()
+    t.frame(timing=False)
+    assert np.array_equal(t.read(TN.MASK), logpolar_mask_np(W, H, W // 2, H - H // 2, signed=True))
 
 
 def test_composite_views_side_by_side(fovrt_mod):
@@ -667,7 +694,7 @@ def test_logpolar_mask_cache_follows_the_gaze(fovrt_mod):
     for gaze_window in (None, None, (40.0, 30.0), (40.0, 30.0), (150.0, 90.0)):
         if gaze_window is not None:
             t.set_gaze(*gaze_window)
-            g = (np.float32(gaze_window[0]), np.float32(H) - np.float32(gaze_window[1]))
+            g = ref_gaze(H, *gaze_window)
         else:
             g = (W // 2, H - H // 2)
         t.frame(timing=False)
@@ -734,3 +761,92 @@ def test_gpu_bvh_follows_moved_triangles(fovrt_mod, oracle):
     assert np.array_equal(t.scene_arrays()["pos"].reshape(-1, 3, 3), pos)
     t.geometry_launch()
     assert equal_nan(t.read(TN.POSITION), ref["position"])
+
+
+# ---------------------------------------------------------------------------------------------
+# Multi-GPU groups through the C ABI (fr_group_*): ranks as contexts of this process on the one GPU
+# of the box (device-to-device copies), and a one-rank RCCL communicator. The group runs the same
+# frame as the reference's loop on one GPU, so every output equals the single-context frame.
+# ---------------------------------------------------------------------------------------------
+GROUP_CASES = [  # (ranks, views, tile, split, moving, W, H, mask)
+    (2, 1, 64, True, False, 200, 136, 4), (3, 1, 32, True, False, 200, 136, 4), (4, 1, 16, True, False, 200, 136, 0),
+    (3, 1, 32, False, False, 200, 136, 4), (4, 2, 32, True, False, 200, 136, 4), (2, 1, 32, True, True, 160, 112, 0),
+    (3, 1, 16, True, True, 160, 112, 4), (4, 1, 128, True, False, 3840, 2160, 4)]
+
+
+@pytest.mark.parametrize("R,V,tile,split,moving,W,H,mask", GROUP_CASES)
+def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving, W, H, mask):
+    """fr_group_frame over R in-process ranks (V views of G = R / V): pipelined frames (no host sync but
+    each rank's own front stages); with moving=True the camera pans every frame and every rank receives
+    every other rank's traced pixels. Each view's reconstruction ranks hold the single-context frame's
+    SHADING and history, view rank 0 its JFA / Sibson and the output rank its pull-push / A-Trous; the
+    composite on rank 0 is the views' A-Trous images side by side."""
+    import torch
+    G = R // V
+    mk = lambda: make_tracer(fovrt_mod, W, H, scene=1, mask=mask, spp=4, dmd=3)
+    ranks = [mk() for _ in range(R)]
+    fulls = [mk() for _ in range(V)]
+    cams = []
+    for v in range(V):
+        cam = fovrt_mod.Camera.preset(1, W, H)
+        cam.setPosition(np.asarray(cam.pos) + np.array([0.064 * (v - (V - 1) / 2), 0, 0], np.float32))
+        cam.lookAt(cam.target)
+        cams.append(cam)
+    g = fovrt_mod.Group(ranks, views=V, tile=tile, split_recon=split, moving_camera=moving, composite=True)
+    info = [g.rank_info(i) for i in range(R)]
+    assert sum(i["tiles"] for i in info[:G]) == ((W + tile - 1) // tile) * ((H + tile - 1) // tile)
+    for f in range(4):
+        for v in range(V):
+            if moving:
+                cams[v].setPrevState()
+                cams[v].lookAt(np.asarray(cams[v].target) + np.array([0.02, 0.01, 0.0], np.float32))
+            fulls[v].update_optix_variables(cams[v])
+            for r in range(v * G, (v + 1) * G):
+                ranks[r].update_optix_variables(cams[v])
+            fulls[v].frame(timing=False)
+        g.frame(timing=(f == 2))
+    g.synchronize()
+    out = torch.empty(V * W * H * 4, dtype=torch.float32, device="cuda")
+    g.composite(out.data_ptr(), out.numel() * 4)
+    comp = out.cpu().numpy().reshape(H, V * W, 4)
+    for v in range(V):
+        full = fulls[v]
+        for r in range(v * G, (v + 1) * G):
+            ch = info[r]["chains"]
+            if ch or moving:
+                for tid in (TN.SHADING, TN.HISTORY_CACHE):
+                    assert equal_nan(ranks[r].read(tid), full.read(tid)), (v, r, tid)
+            if ch & 1:
+                for tid in (TN.JFA_COLOR, TN.SIBSON):
+                    assert equal_nan(ranks[r].read(tid), full.read(tid)), (v, r, tid)
+            if ch & 2:
+                for tid in (TN.PULLPUSH, TN.ATROUS):
+                    assert equal_nan(ranks[r].read(tid), full.read(tid)), (v, r, tid)
+        assert equal_nan(comp[:, v * W:(v + 1) * W], full.read(TN.ATROUS)), v
+        chains = [info[r]["chains"] for r in range(v * G, (v + 1) * G)]
+        assert chains[0] & 1 and any(c & 2 for c in chains)
+    g.destroy()
+    for t in ranks + fulls:
+        t.destroy()
+
+
+def test_group_one_rank_rccl(fovrt_mod):
+    """A one-rank RCCL communicator (fr_rccl_unique_id / fr_rccl_comm_init) driving a group with the
+    composite: the group frame equals fr_frame and the composite is the A-Trous image."""
+    import torch
+    W, H = 128, 96
+    t = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    full = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    uid = fovrt_mod.rccl_unique_id()
+    assert len(uid) == 128
+    g = fovrt_mod.Group.rccl(t, uid, 1, 0, composite=True)
+    assert g.rank_info(0) == {"view": 0, "view_rank": 0, "chains": 3, "tiles": ((W + 127) // 128) * ((H + 127) // 128)}
+    for _ in range(3):
+        g.frame()
+        full.frame(timing=False)
+    out = torch.empty(W * H * 4, dtype=torch.float32, device="cuda")
+    g.composite(out.data_ptr(), out.numel() * 4)
+    for tid in (TN.SHADING, TN.SIBSON, TN.ATROUS):
+        assert equal_nan(t.read(tid), full.read(tid)), tid
+    assert equal_nan(out.cpu().numpy().reshape(H, W, 4), full.read(TN.ATROUS))
+    g.destroy()
