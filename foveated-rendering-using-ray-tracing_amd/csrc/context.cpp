@@ -1130,6 +1130,10 @@ int fr_get_buffer(fr_ctx* c, int id, fr_buffer_view* v) {
     *v = fr_buffer_view{c->mask, c->W, c->H, (size_t)c->W, N, FR_FMT_U8};
     return FR_OK;
   }
+  if (id == FR_BUF_GCLASS) {
+    *v = fr_buffer_view{c->gclass, c->W, c->H, (size_t)c->W, N, FR_FMT_U8};
+    return FR_OK;
+  }
   int p;
   if (resolve(c, id, &p)) return fail(c, FR_E_INVALID, "unknown buffer id");
   *v = fr_buffer_view{c->img[p], c->W, c->H, (size_t)c->W * sizeof(f4), N * sizeof(f4), FR_FMT_RGBA32F};

@@ -40,7 +40,7 @@ class TextureName:
     """PathTracer::TextureName (FR/PathTracer.h:13-31) plus the reconstruction outputs."""
     POSITION, NORMAL, DEPTH, DIFFUSE, WEIGHT, THREAD, HISTORY, SHADING, EXTRA = range(9)
     JFA_COORD, JFA_COLOR, SIBSON, PULLPUSH, ATROUS, DEPTH_CACHE, HISTORY_CACHE, MASK = range(9, 17)
-    LOGPOLAR, LOGPOLAR_INVERSE = 17, 18
+    LOGPOLAR, LOGPOLAR_INVERSE, GCLASS = 17, 18, 19
 
 
 class FovrtError(RuntimeError):

@@ -122,7 +122,9 @@ typedef enum fr_buffer_id {
   FR_BUF_MASK = 16,         /* u8 usingRay per pixel */
   FR_BUF_LOGPOLAR = 17,     /* LogPolarTransform::logPolarTex  (forward image, W/4 x H/4 used) */
   FR_BUF_LOGPOLAR_INVERSE = 18, /* LogPolarTransform::ilogPolarTex */
-  FR_BUF_COUNT = 19
+  FR_BUF_GCLASS = 19,       /* u8 primary-hit class of the last G-buffer: 0 refraction, 1 reflection, 2 diffuse,
+                             * 3 miss (the megakernel's class-major work order; diagnostics) */
+  FR_BUF_COUNT = 20
 } fr_buffer_id;
 
 typedef enum fr_format { FR_FMT_RGBA32F = 0, FR_FMT_U32 = 1, FR_FMT_U8 = 2 } fr_format;
