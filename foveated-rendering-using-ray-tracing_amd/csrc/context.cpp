@@ -248,50 +248,50 @@ int fr_camera_uniforms(const fr_camera_pose* cur, const fr_camera_pose* prev, in
   return FR_OK;
 }
 
-// GPU build over c->d_pos (k_bvh.hip): replaces the device BVH arrays and mirrors them into
-// c->bvh (fr_scene_export).
+// GPU build over c->d_pos (k_bvh.hip) into the spare arrays, which become the scene's tree when every
+// step succeeded (the old tree becomes the spare). No allocation after the first rebuild, no read-back
+// of the tree: the host keeps its node count, stack need and depth (fr_scene_export).
 static int gpu_rebuild(fr_ctx* c) {
   const int nt = c->scene.num_tris();
-  BvhNode* nodes = nullptr;
-  TriGeo* tri = nullptr;
-  int32_t* prim = nullptr;
-  int nn = 0, max_stack = 0;
+  if (!c->spare_nodes) {  // (a failed re-allocation below left none)
+    if (hipMalloc((void**)&c->spare_nodes, (size_t)std::max(nt, 1) * sizeof(BvhNode)) != hipSuccess ||
+        hipMalloc((void**)&c->spare_tri, (size_t)std::max(nt, 1) * sizeof(TriGeo)) != hipSuccess ||
+        hipMalloc((void**)&c->spare_prim, (size_t)std::max(nt, 1) * sizeof(int32_t)) != hipSuccess) {
+      c->err = "GPU BVH: device allocation failed";
+      return FR_E_NOMEM;
+    }
+  }
+  int nn = 0, max_stack = 0, depth = 0;
   std::string err;
-  if (!gpu_build_bvh(c->d_pos, nt, &nodes, &tri, &prim, &nn, &max_stack, c->stream, err)) {
+  if (!gpu_build_bvh(&c->bvh_work, c->d_pos, nt, c->spare_nodes, c->spare_tri, c->spare_prim, &nn, &max_stack, &depth,
+                     c->stream, err)) {
     c->err = err;
     return FR_E_HIP;
   }
   if (max_stack > FR_BVH_STACK) {
-    hipFree(nodes); hipFree(tri); hipFree(prim);
     c->err = "GPU BVH needs a traversal stack deeper than FR_BVH_STACK";
     return FR_E_UNSUPPORTED;
   }
-  // host mirror first: the context switches to the new tree only when every step succeeded
+  std::swap(c->d_nodes, c->spare_nodes);
+  std::swap(c->d_tri, c->spare_tri);
+  std::swap(c->d_prim, c->spare_prim);
+  if (!c->tree_full_cap) {
+    // the replaced tree was sized for the host builder's node count (or there was none): the next spare
+    // needs room for any device-built tree (at most one node per triangle)
+    if (c->spare_nodes) { hipFree(c->spare_nodes); hipFree(c->spare_tri); hipFree(c->spare_prim); }
+    c->spare_nodes = nullptr; c->spare_tri = nullptr; c->spare_prim = nullptr;
+    c->tree_full_cap = true;
+    if (hipMalloc((void**)&c->spare_nodes, (size_t)std::max(nt, 1) * sizeof(BvhNode)) != hipSuccess ||
+        hipMalloc((void**)&c->spare_tri, (size_t)std::max(nt, 1) * sizeof(TriGeo)) != hipSuccess ||
+        hipMalloc((void**)&c->spare_prim, (size_t)std::max(nt, 1) * sizeof(int32_t)) != hipSuccess) {
+      hipFree(c->spare_nodes); hipFree(c->spare_tri); hipFree(c->spare_prim);
+      c->spare_nodes = nullptr; c->spare_tri = nullptr; c->spare_prim = nullptr;  // allocated again next time
+    }
+  }
+  c->dsc.nodes = c->d_nodes; c->dsc.tri_geo = c->d_tri; c->dsc.tri_prim = c->d_prim;
   Bvh b;
-  b.nodes.resize(nn); b.tri_geo.resize(nt); b.tri_prim.resize(nt);
-  b.root_count = 0; b.max_stack = max_stack; b.max_depth = 0;
-  if (hipMemcpy(b.nodes.data(), nodes, (size_t)nn * sizeof(BvhNode), hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(b.tri_geo.data(), tri, (size_t)nt * sizeof(TriGeo), hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(b.tri_prim.data(), prim, (size_t)nt * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) {
-    hipFree(nodes); hipFree(tri); hipFree(prim);
-    c->err = "GPU BVH: readback failed";
-    return FR_E_HIP;
-  }
-  if (c->d_nodes) hipFree(c->d_nodes);
-  if (c->d_tri) hipFree(c->d_tri);
-  if (c->d_prim) hipFree(c->d_prim);
-  c->d_nodes = nodes; c->d_tri = tri; c->d_prim = prim;
-  c->dsc.nodes = nodes; c->dsc.tri_geo = tri; c->dsc.tri_prim = prim;
-  // tree depth (fr_scene_info.bvh_depth) of the four-wide tree: the inner entries have count 0
-  std::vector<std::pair<int, int>> todo{{0, 0}};
-  while (!todo.empty()) {
-    const auto [ni, depth] = todo.back();
-    todo.pop_back();
-    b.max_depth = std::max(b.max_depth, depth);
-    for (int k = 0; k < 4; k++)
-      if (b.nodes[ni].count[k] == 0 && b.nodes[ni].child[k] > ni && b.nodes[ni].child[k] < nn)
-        todo.push_back({b.nodes[ni].child[k], depth + 1});
-  }
+  b.root_count = 0; b.max_stack = max_stack; b.max_depth = depth;
+  b.gpu_nodes = nn;
   c->bvh = std::move(b);
   return FR_OK;
 }
@@ -389,10 +389,30 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     c->err = "device allocation (scene) failed";
     return bail(FR_E_NOMEM);
   }
-  if (cfg.bvh_builder == 0) {
-    if (!up(&c->d_nodes, c->bvh.nodes) || !up(&c->d_tri, c->bvh.tri_geo) || !up(&c->d_prim, c->bvh.tri_prim)) {
+  // The tree arrays hold one entry per triangle (room for any device-built tree), and the GPU builder's
+  // spare arrays and scratch exist from the start: fr_rebuild_bvh allocates nothing (hipMalloc / hipFree
+  // in a rebuild cost ~10-20 ms and synchronise the device).
+  {
+    const size_t cap = (size_t)std::max(nt, 1);
+    if (hipMalloc((void**)&c->d_nodes, std::max(cap, c->bvh.nodes.size()) * sizeof(BvhNode)) != hipSuccess ||
+        hipMalloc((void**)&c->d_tri, cap * sizeof(TriGeo)) != hipSuccess ||
+        hipMalloc((void**)&c->d_prim, cap * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc((void**)&c->spare_nodes, cap * sizeof(BvhNode)) != hipSuccess ||
+        hipMalloc((void**)&c->spare_tri, cap * sizeof(TriGeo)) != hipSuccess ||
+        hipMalloc((void**)&c->spare_prim, cap * sizeof(int32_t)) != hipSuccess) {
       c->err = "device allocation (scene) failed";
       return bail(FR_E_NOMEM);
+    }
+    c->tree_full_cap = c->bvh.nodes.size() <= cap;
+    std::string werr;
+    if (nt >= 3 && !bvh_work_prepare(&c->bvh_work, nt, c->stream, werr)) { c->err = werr; return bail(FR_E_NOMEM); }
+  }
+  if (cfg.bvh_builder == 0) {
+    if (hipMemcpy(c->d_nodes, c->bvh.nodes.data(), c->bvh.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_tri, c->bvh.tri_geo.data(), c->bvh.tri_geo.size() * sizeof(TriGeo), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_prim, c->bvh.tri_prim.data(), c->bvh.tri_prim.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) {
+      c->err = "device copy (scene) failed";
+      return bail(FR_E_HIP);
     }
   } else if (int rc = gpu_rebuild(c)) {
     return bail(rc);
@@ -450,6 +470,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, std::max(N * cfg.spp, 2 * shade_fx_slots((uint32_t)N, cfg.spp, c->handoff))) != hipSuccess ||
       dalloc(&c->sample_help, std::max<size_t>(4 * shade_fx_slots((uint32_t)N, cfg.spp, c->handoff), 1)) != hipSuccess ||
       dalloc(&c->aux, N) != hipSuccess || dalloc(&c->aux_seed, N) != hipSuccess ||
+      hipMalloc((void**)&c->item_store, shade_item_store_f4() * sizeof(f4)) != hipSuccess ||
       (cfg.sibson_mode == 0 && (dalloc(&c->sib_prefix, (size_t)(c->W + 1) * c->H) != hipSuccess ||
                                 dalloc(&c->sib_blocks, (size_t)sibson_prefix_blocks(c->W) * c->H) != hipSuccess))) {
     c->err = "device allocation (work buffers) failed";
@@ -501,6 +522,8 @@ int fr_destroy(fr_ctx* c) {
   if (c->stream5) hipStreamSynchronize(c->stream5);
   auto fr = [](void* p) { if (p) hipFree(p); };
   fr(c->d_nodes); fr(c->d_tri); fr(c->d_prim); fr(c->d_shade); fr(c->d_pos);
+  fr(c->spare_nodes); fr(c->spare_tri); fr(c->spare_prim);
+  if (c->bvh_work) bvh_work_free(c->bvh_work);
   for (auto p : c->d_tex) fr(p);
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
@@ -508,7 +531,7 @@ int fr_destroy(fr_ctx* c) {
   fr(c->bcount); fr(c->shard_map);
   if (c->h_counts) hipHostFree(c->h_counts);
   for (auto e : c->ev_counts) if (e) hipEventDestroy(e);
-  fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
+  fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->item_store); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->ev_front) hipEventDestroy(c->ev_front);
@@ -668,7 +691,7 @@ static int enqueue_shading(fr_ctx* c) {
   if (kt) hipEventRecord(kt[1], c->stream);
   launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache],
                      c->shade_ctr, c->samples, c->sample_help, c->stats, c->aux, c->aux_seed, c->chunk_refr,
-                     c->xcd_bands, c->handoff, c->stream);
+                     c->xcd_bands, c->handoff, c->item_store, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   if (kt) hipEventRecord(kt[2], c->stream);
   hipStreamWaitEvent(c->stream, c->ev[12], 0);
@@ -928,6 +951,49 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
 }
 
 int fr_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, true, true); }
+int fr_set_sample_sum(fr_ctx* c, int mode) {
+  if (!c) return FR_E_INVALID;
+  if (mode < 0 || mode > 2) return fail(c, FR_E_INVALID, "fr_set_sample_sum: mode 0 (fp32), 1 (by frame size) or 2 (fixed point)");
+  if ((uint32_t)mode == c->handoff) return FR_OK;
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  HIP_TRY(c, hipDeviceSynchronize());
+  // the fixed-point form keeps 32-B sample records and a 32-B help record per sample
+  const size_t N = (size_t)c->W * c->H;
+  const size_t need_s = std::max(N * c->cfg.spp, 2 * shade_fx_slots((uint32_t)N, c->cfg.spp, (uint32_t)mode));
+  const size_t need_h = std::max<size_t>(4 * shade_fx_slots((uint32_t)N, c->cfg.spp, (uint32_t)mode), 1);
+  const size_t have_s = std::max(N * c->cfg.spp, 2 * shade_fx_slots((uint32_t)N, c->cfg.spp, c->handoff));
+  const size_t have_h = std::max<size_t>(4 * shade_fx_slots((uint32_t)N, c->cfg.spp, c->handoff), 1);
+  if (need_s > have_s) {
+    hipFree(c->samples); c->samples = nullptr;
+    if (dalloc(&c->samples, need_s) != hipSuccess) return fail(c, FR_E_NOMEM, "fr_set_sample_sum: allocation failed");
+  }
+  if (need_h > have_h) {
+    hipFree(c->sample_help); c->sample_help = nullptr;
+    if (dalloc(&c->sample_help, need_h) != hipSuccess) return fail(c, FR_E_NOMEM, "fr_set_sample_sum: allocation failed");
+  }
+  c->handoff = (uint32_t)mode;
+  return FR_OK;
+}
+
+int fr_shard_unpack_active_enqueue(fr_ctx* c, const void* slab, size_t slab_bytes, uint32_t capacity, uint32_t count) {
+  if (!c || !slab) return FR_E_INVALID;
+  if (count > capacity) return fail(c, FR_E_INVALID, "fr_shard_unpack_active: count above capacity");
+  if (slab_bytes < (size_t)capacity * 20) return fail(c, FR_E_INVALID, "fr_shard_unpack_active: slab smaller than 20 * capacity");
+  hipSetDevice(c->cfg.device);
+  const f4* vals = (const f4*)slab;
+  const uint32_t* idx = (const uint32_t*)((const char*)slab + (size_t)capacity * sizeof(f4));
+  launch_shard_unpack_active(vals, idx, count, (uint32_t)((size_t)c->W * c->H), c->img[c->hist_cache], c->img[P_shd(c)],
+                             c->stream);
+  return check_launch(c);
+}
+
+int fr_set_recon_chains(fr_ctx* c, int chains) {
+  if (!c) return FR_E_INVALID;
+  if (chains < 0 || chains > 3) return fail(c, FR_E_INVALID, "fr_set_recon_chains: chains is a mask of bits 0 and 1");
+  c->recon_chains = chains;
+  return FR_OK;
+}
 int fr_trace_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, true, false); }
 int fr_reconstruct_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, false, true); }
 
@@ -1389,7 +1455,7 @@ static void fill_arrays(const HostScene& s, const Bvh& bvh, f3 emission, std::ve
   for (int i = 0; i < 5; i++) { o->light[3 * i] = L[i].x; o->light[3 * i + 1] = L[i].y; o->light[3 * i + 2] = L[i].z; }
   o->bbox[0] = s.bbox_min.x; o->bbox[1] = s.bbox_min.y; o->bbox[2] = s.bbox_min.z;
   o->bbox[3] = s.bbox_max.x; o->bbox[4] = s.bbox_max.y; o->bbox[5] = s.bbox_max.z;
-  o->bvh_nodes = (int)bvh.nodes.size();
+  o->bvh_nodes = bvh.gpu_nodes >= 0 ? bvh.gpu_nodes : (int)bvh.nodes.size();
   o->bvh_depth = bvh.max_depth;
   o->bvh_max_stack = bvh.max_stack;
 }

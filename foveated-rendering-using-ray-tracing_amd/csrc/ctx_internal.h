@@ -16,7 +16,8 @@ namespace fr {
 void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
 void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
                         const f4*, uint32_t*, f4*, unsigned long long*, DevStats*, f4*, uint32_t*, uint32_t, uint32_t,
-                        uint32_t, hipStream_t);
+                        uint32_t, f4*, hipStream_t);
+size_t shade_item_store_f4();
 void launch_sample_setup(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*, f4*,
                          uint32_t*, hipStream_t);
 void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
@@ -42,7 +43,10 @@ void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, hipStream
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
 void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, int, int, hipStream_t);
 int sibson_prefix_blocks(int W);
-bool gpu_build_bvh(const f3*, int, BvhNode**, TriGeo**, int32_t**, int*, int*, hipStream_t, std::string&);
+struct BvhWork;
+bool gpu_build_bvh(BvhWork**, const f3*, int, BvhNode*, TriGeo*, int32_t*, int*, int*, int*, hipStream_t, std::string&);
+void bvh_work_free(BvhWork*);
+bool bvh_work_prepare(BvhWork**, int, hipStream_t, std::string&);
 #ifdef FR_STAMPS
 void launch_trace_queries(const DevScene&, const f4*, uint32_t, f4*, uint32_t*, hipStream_t, int);
 void diag_record_queries(f4*, uint32_t, hipStream_t);
@@ -136,6 +140,12 @@ struct fr_ctx {
   f3* d_pos = nullptr;  // world-space vertices, 3 per triangle (the GPU builder's input)
   TriGeo* d_tri = nullptr;
   int32_t* d_prim = nullptr;
+  // the GPU builder's target arrays (swapped with the current tree after a successful build) and its scratch
+  BvhNode* spare_nodes = nullptr;
+  TriGeo* spare_tri = nullptr;
+  int32_t* spare_prim = nullptr;
+  fr::BvhWork* bvh_work = nullptr;
+  bool tree_full_cap = false;  // d_nodes / d_tri / d_prim hold one entry per triangle (a device-built tree)
   TriShade* d_shade = nullptr;
   std::vector<f4*> d_tex;
   DevMaterial* d_mats = nullptr;
@@ -160,6 +170,7 @@ struct fr_ctx {
   uint32_t* shade_ctr = nullptr;  // sharded chunk counters of the shading work queue
   f4* samples = nullptr;          // one radiance value per (active pixel, camera sample): 16 B, or 32 B fixed point
   unsigned long long* sample_help = nullptr;  // fixed-point shares of the lanes that took over items, 32 B per sample
+  f4* item_store = nullptr;     // the megakernel's refraction item stacks (shade_item_store_f4)
   f4* aux = nullptr;              // per active pixel: NDC position, r1, r2 (k_sample_setup)
   uint32_t* aux_seed = nullptr;   // per active pixel: the seed after the two draws
   u2 *jfa_a = nullptr, *jfa_b = nullptr;  // JFA state ping-pong (seed coord texel + alpha flags)

@@ -198,9 +198,11 @@ struct BinTree {
 // now (k_emit_leaves relays them out).
 __global__ void k_collapse(BinTree T, const CollapseItem* __restrict__ cur, const uint32_t* __restrict__ ncur,
                            CollapseItem* __restrict__ next, uint32_t* __restrict__ nnext, uint32_t* __restrict__ node_ctr,
-                           BvhNode* __restrict__ nodes, uint32_t* __restrict__ max_stack) {
+                           BvhNode* __restrict__ nodes, uint32_t* __restrict__ max_stack, uint32_t* __restrict__ levels) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *ncur) return;
+  const uint32_t nc = *ncur;
+  if (i == 0 && nc) atomicAdd(levels, 1u);
+  if (i >= nc) return;
   const CollapseItem it = cur[i];
   int e[4];
   int ne = 2;
@@ -296,13 +298,10 @@ hipError_t alloc(T** p, size_t n) {
 
 }  // namespace
 
-// Builds the four-wide BVH of n triangles (pos: 3 vertices per triangle, device) into nodes / tri
-// / prim (device, allocated here, n entries each; the caller frees them). Returns false with err
-// set on failure. num_nodes and max_stack describe the result.
-bool gpu_build_bvh(const f3* pos, int n, BvhNode** nodes_out, TriGeo** tri_out, int32_t** prim_out, int* num_nodes,
-                   int* max_stack, hipStream_t s, std::string& err) {
-  *nodes_out = nullptr; *tri_out = nullptr; *prim_out = nullptr;
-  if (n < 3) { err = "GPU BVH builder needs at least 3 triangles"; return false; }
+// Scratch of the builder, kept by the context between rebuilds (no allocation, no hipFree, which would
+// synchronise the whole device, in a rebuild once it exists).
+struct BvhWork {
+  int cap = 0;
   f4 *blo = nullptr, *bhi = nullptr, *nlo = nullptr, *nhi = nullptr;
   uint32_t *cb = nullptr, *codes = nullptr, *codes_s = nullptr, *arrivals = nullptr, *ctr = nullptr, *cnt = nullptr,
            *off = nullptr;
@@ -311,72 +310,108 @@ bool gpu_build_bvh(const f3* pos, int n, BvhNode** nodes_out, TriGeo** tri_out, 
   int* parent = nullptr;
   CollapseItem *qa = nullptr, *qb = nullptr;
   void* tmp = nullptr;
-  bool ok = false;
-  do {
-    if (alloc(&blo, n) || alloc(&bhi, n) || alloc(&nlo, n) || alloc(&nhi, n) || alloc(&cb, 6) || alloc(&codes, n) ||
-        alloc(&codes_s, n) || alloc(&ids, n) || alloc(&ids_s, n) || alloc(&child, n) || alloc(&range, n) ||
-        alloc(&parent, 2 * n) || alloc(&arrivals, n) || alloc(&ctr, 4) || alloc(&qa, n) || alloc(&qb, n) ||
-        alloc(&cnt, n) || alloc(&off, n) || alloc(nodes_out, n) || alloc(tri_out, n) || alloc(prim_out, n)) {
-      err = "GPU BVH builder: device allocation failed";
-      break;
-    }
-    const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
-    hipMemcpyAsync(cb, init, sizeof(init), hipMemcpyHostToDevice, s);
-    const int B = 256, G = (n + B - 1) / B;
-    hipLaunchKernelGGL(k_prim_boxes, dim3(std::min(G, 2048)), dim3(B), 0, s, pos, n, blo, bhi, cb);
-    hipLaunchKernelGGL(k_morton, dim3(G), dim3(B), 0, s, blo, bhi, n, cb, codes, ids);
-    size_t tmp_bytes = 0, scan_bytes = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, codes, codes_s, ids, ids_s, n, 0, 30, s);
-    hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, cnt, off, n, s);
-    if (hipMalloc(&tmp, std::max(tmp_bytes, scan_bytes))) { err = "GPU BVH builder: scratch allocation failed"; break; }
-    hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, codes, codes_s, ids, ids_s, n, 0, 30, s);
-    hipLaunchKernelGGL(k_karras, dim3(G), dim3(B), 0, s, codes_s, n, child, parent, range);
-    hipMemsetAsync(arrivals, 0, (size_t)n * sizeof(uint32_t), s);
-    hipLaunchKernelGGL(k_boxes_up, dim3(G), dim3(B), 0, s, n, ids_s, blo, bhi, parent, child, nlo, nhi, arrivals);
-    // collapse, one launch per level of the four-wide tree
-    BinTree T{n, child, range, nlo, nhi, blo, bhi, ids_s};
-    const CollapseItem root{0, 0, 0};
-    const uint32_t ctr_init[4] = {1u, 0u, 1u, 0u};  // node_ctr, max_stack, ncur, nnext
-    hipMemcpyAsync(qa, &root, sizeof(root), hipMemcpyHostToDevice, s);
-    hipMemcpyAsync(ctr, ctr_init, sizeof(ctr_init), hipMemcpyHostToDevice, s);
-    uint32_t ncur = 1;
-    int levels = 0;
-    while (ncur) {
-      hipMemsetAsync(ctr + 3, 0, sizeof(uint32_t), s);
-      hipLaunchKernelGGL(k_collapse, dim3((ncur + B - 1) / B), dim3(B), 0, s, T, qa, ctr + 2, qb, ctr + 3, ctr,
-                         *nodes_out, ctr + 1);
-      hipMemcpyAsync(ctr + 2, ctr + 3, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
-      hipMemcpyAsync(&ncur, ctr + 3, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-      hipStreamSynchronize(s);
-      std::swap(qa, qb);
-      if (++levels > 64) break;
-    }
-    if (ncur) { err = "GPU BVH builder: collapse did not terminate"; break; }
-    uint32_t h[2];
-    hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-    *num_nodes = (int)h[0];
-    *max_stack = (int)h[1];
-    const int nn = *num_nodes, GN = (nn + B - 1) / B;
-    hipLaunchKernelGGL(k_leaf_counts, dim3(GN), dim3(B), 0, s, *nodes_out, nn, cnt);
-    hipcub::DeviceScan::ExclusiveSum(tmp, scan_bytes, cnt, off, nn, s);
-    hipLaunchKernelGGL(k_emit_leaves, dim3(GN), dim3(B), 0, s, *nodes_out, nn, off, ids_s, pos, *tri_out, *prim_out);
-    if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) {
-      err = "GPU BVH builder: kernel failure";
-      break;
-    }
-    ok = true;
-  } while (false);
-  for (void* p : {(void*)blo, (void*)bhi, (void*)nlo, (void*)nhi, (void*)cb, (void*)codes, (void*)codes_s, (void*)ids,
-                  (void*)ids_s, (void*)child, (void*)range, (void*)parent, (void*)arrivals, (void*)ctr, (void*)qa,
-                  (void*)qb, (void*)cnt, (void*)off, tmp})
+  size_t tmp_bytes = 0;
+  uint32_t* host = nullptr;  // pinned: ncur, node count, max stack, levels
+};
+
+void bvh_work_free(BvhWork* w) {
+  if (!w) return;
+  for (void* p : {(void*)w->blo, (void*)w->bhi, (void*)w->nlo, (void*)w->nhi, (void*)w->cb, (void*)w->codes,
+                  (void*)w->codes_s, (void*)w->ids, (void*)w->ids_s, (void*)w->child, (void*)w->range, (void*)w->parent,
+                  (void*)w->arrivals, (void*)w->ctr, (void*)w->qa, (void*)w->qb, (void*)w->cnt, (void*)w->off, w->tmp})
     if (p) hipFree(p);
-  if (!ok) {
-    for (void* p : {(void*)*nodes_out, (void*)*tri_out, (void*)*prim_out})
-      if (p) hipFree(p);
-    *nodes_out = nullptr; *tri_out = nullptr; *prim_out = nullptr;
+  if (w->host) hipHostFree(w->host);
+  delete w;
+}
+
+static bool bvh_work_reserve(BvhWork*& w, int n, hipStream_t s, std::string& err) {
+  if (w && w->cap >= n) return true;
+  bvh_work_free(w);
+  w = new BvhWork();
+  if (alloc(&w->blo, n) || alloc(&w->bhi, n) || alloc(&w->nlo, n) || alloc(&w->nhi, n) || alloc(&w->cb, 6) ||
+      alloc(&w->codes, n) || alloc(&w->codes_s, n) || alloc(&w->ids, n) || alloc(&w->ids_s, n) || alloc(&w->child, n) ||
+      alloc(&w->range, n) || alloc(&w->parent, 2 * n) || alloc(&w->arrivals, n) || alloc(&w->ctr, 8) ||
+      alloc(&w->qa, n) || alloc(&w->qb, n) || alloc(&w->cnt, n) || alloc(&w->off, n) ||
+      hipHostMalloc((void**)&w->host, 8 * sizeof(uint32_t)) != hipSuccess) {
+    err = "GPU BVH builder: device allocation failed";
+    bvh_work_free(w);
+    w = nullptr;
+    return false;
   }
-  return ok;
+  size_t sort_bytes = 0, scan_bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, w->codes, w->codes_s, w->ids, w->ids_s, n, 0, 30, s);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, w->cnt, w->off, n, s);
+  w->tmp_bytes = std::max(sort_bytes, scan_bytes);
+  if (hipMalloc(&w->tmp, w->tmp_bytes) != hipSuccess) {
+    err = "GPU BVH builder: scratch allocation failed";
+    bvh_work_free(w);
+    w = nullptr;
+    return false;
+  }
+  w->cap = n;
+  return true;
+}
+
+bool bvh_work_prepare(BvhWork** w, int n, hipStream_t s, std::string& err) { return bvh_work_reserve(*w, n, s, err); }
+
+// Builds the four-wide BVH of n triangles (pos: 3 vertices per triangle, device) into the caller's
+// nodes / tri / prim (device, n entries each) with the workspace *work (created or grown here, kept
+// by the caller). Returns false with err set on failure. num_nodes, max_stack and depth (levels of
+// the four-wide tree below the root) describe the result. The collapse runs its levels in batches of
+// launches that skip themselves once the level queue is empty, with one host read per batch.
+bool gpu_build_bvh(BvhWork** work, const f3* pos, int n, BvhNode* nodes, TriGeo* tri, int32_t* prim, int* num_nodes,
+                   int* max_stack, int* depth, hipStream_t s, std::string& err) {
+  if (n < 3) { err = "GPU BVH builder needs at least 3 triangles"; return false; }
+  if (!bvh_work_reserve(*work, n, s, err)) return false;
+  BvhWork& w = **work;
+  const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+  hipMemcpyAsync(w.cb, init, sizeof(init), hipMemcpyHostToDevice, s);
+  const int B = 256, G = (n + B - 1) / B;
+  hipLaunchKernelGGL(k_prim_boxes, dim3(std::min(G, 2048)), dim3(B), 0, s, pos, n, w.blo, w.bhi, w.cb);
+  hipLaunchKernelGGL(k_morton, dim3(G), dim3(B), 0, s, w.blo, w.bhi, n, w.cb, w.codes, w.ids);
+  size_t tb = w.tmp_bytes;
+  hipcub::DeviceRadixSort::SortPairs(w.tmp, tb, w.codes, w.codes_s, w.ids, w.ids_s, n, 0, 30, s);
+  hipLaunchKernelGGL(k_karras, dim3(G), dim3(B), 0, s, w.codes_s, n, w.child, w.parent, w.range);
+  hipMemsetAsync(w.arrivals, 0, (size_t)n * sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_boxes_up, dim3(G), dim3(B), 0, s, n, w.ids_s, w.blo, w.bhi, w.parent, w.child, w.nlo, w.nhi,
+                     w.arrivals);
+  BinTree T{n, w.child, w.range, w.nlo, w.nhi, w.blo, w.bhi, w.ids_s};
+  const CollapseItem root{0, 0, 0};
+  // ctr: node_ctr, max_stack, ncur, nnext, levels
+  const uint32_t ctr_init[5] = {1u, 0u, 1u, 0u, 0u};
+  hipMemcpyAsync(w.qa, &root, sizeof(root), hipMemcpyHostToDevice, s);
+  hipMemcpyAsync(w.ctr, ctr_init, sizeof(ctr_init), hipMemcpyHostToDevice, s);
+  const int kBatch = 8;
+  int launched = 0;
+  CollapseItem *qa = w.qa, *qb = w.qb;
+  for (;;) {
+    for (int b = 0; b < kBatch; b++) {
+      hipMemsetAsync(w.ctr + 3, 0, sizeof(uint32_t), s);
+      // a level holds at most n items (one per inner node of the binary tree)
+      hipLaunchKernelGGL(k_collapse, dim3(G), dim3(B), 0, s, T, qa, w.ctr + 2, qb, w.ctr + 3, w.ctr, nodes, w.ctr + 1,
+                         w.ctr + 4);
+      hipMemcpyAsync(w.ctr + 2, w.ctr + 3, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
+      std::swap(qa, qb);
+    }
+    launched += kBatch;
+    hipMemcpyAsync(w.host, w.ctr, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    if (hipStreamSynchronize(s) != hipSuccess) { err = "GPU BVH builder: kernel failure"; return false; }
+    if (w.host[2] == 0) break;
+    if (launched >= 64) { err = "GPU BVH builder: collapse did not terminate"; return false; }
+  }
+  *num_nodes = (int)w.host[0];
+  *max_stack = (int)w.host[1];
+  *depth = (int)w.host[4] - 1;
+  const int nn = *num_nodes, GN = (nn + B - 1) / B;
+  hipLaunchKernelGGL(k_leaf_counts, dim3(GN), dim3(B), 0, s, nodes, nn, w.cnt);
+  tb = w.tmp_bytes;
+  hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.cnt, w.off, nn, s);
+  hipLaunchKernelGGL(k_emit_leaves, dim3(GN), dim3(B), 0, s, nodes, nn, w.off, w.ids_s, pos, tri, prim);
+  if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) {
+    err = "GPU BVH builder: kernel failure";
+    return false;
+  }
+  return true;
 }
 
 }  // namespace fr

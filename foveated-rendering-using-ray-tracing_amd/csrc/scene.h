@@ -40,6 +40,7 @@ struct Bvh {
   int root_count = 0;             // >0 when the root itself is a leaf
   int max_depth = 0;
   int max_stack = 0;              // deepest traversal stack any root-to-leaf path can need
+  int gpu_nodes = -1;             // node count of a device-built tree (its arrays stay on the device)
 };
 
 enum ScenePreset { PRESET_BOX = 0, PRESET_BUNNY = 1, PRESET_VOKSELIA = 2 };

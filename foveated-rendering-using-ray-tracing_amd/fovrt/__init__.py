@@ -138,6 +138,9 @@ _SIGS = {
     "fr_reset_gaze": [C.c_void_p],
     "fr_composite_views": [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
+    "fr_set_recon_chains": [C.c_void_p, C.c_int],
+    "fr_set_sample_sum": [C.c_void_p, C.c_int],
+    "fr_shard_unpack_active_enqueue": [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32],
     "fr_trace_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_reconstruct_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_set_shard": [C.c_void_p, C.c_int, C.c_int, C.c_int],
@@ -475,6 +478,19 @@ class PathTracer:
     def frame(self, timing=True):
         """One iteration of the FR/main.cpp:253-358 loop body on the device."""
         return self._frame(_lib.fr_frame, timing)
+
+    def set_sample_sum(self, mode):
+        """fr_set_sample_sum: 0 fp32, 1 by frame size (default), 2 fixed point with the tail handoff."""
+        self._check(_lib.fr_set_sample_sum(self._ctx, int(mode)))
+
+    def shard_unpack_active_enqueue(self, device_ptr, capacity, count):
+        """fr_shard_unpack_active without synchronisation (enqueued on the context stream)."""
+        self._check(_lib.fr_shard_unpack_active_enqueue(self._ctx, C.c_void_p(device_ptr), int(capacity) * 20,
+                                                        int(capacity), int(count)))
+
+    def set_recon_chains(self, chains):
+        """Reconstruction chains this context runs: bit 0 JFA -> Sibson, bit 1 pull-push -> A-Trous."""
+        self._check(_lib.fr_set_recon_chains(self._ctx, int(chains)))
 
     def trace_frame(self, timing=True):
         """The trace half of a frame (update -> entries 0..3)."""

@@ -226,6 +226,15 @@ int fr_reset_gaze(fr_ctx* ctx);
  * reconstruction, so results are those of the sequential loop. With timing != NULL the frame is
  * synchronised and per-stage HIP-event times are returned. */
 int fr_frame(fr_ctx* ctx, fr_frame_timing* timing);
+/* Which reconstruction chains fr_frame / fr_reconstruct_frame run on this context: bit 0 JumpFlooding ->
+ * Sibson, bit 1 pull-push -> A-Trous (default 3, both; a group's split reconstruction sets 1 and 2 on
+ * the two reconstruction ranks of a view). */
+int fr_set_recon_chains(fr_ctx* ctx, int chains);
+/* How entry 3 sums a camera sample's radiance: 0 fp32 in the oracle's depth-first order,
+ * 1 (default) by frame size (fixed point below 64 pixel-samples per megakernel lane, fp32 above), 2 32.32
+ * fixed point with the tail handoff (idle lanes take pending refraction items of busy ones; the value does
+ * not depend on which lane traces an item). The forms differ by rounding only (<= 1e-4). Synchronises. */
+int fr_set_sample_sum(fr_ctx* ctx, int mode);
 int fr_trace_frame(fr_ctx* ctx, fr_frame_timing* timing);        /* update -> entries 0..3 only */
 int fr_reconstruct_frame(fr_ctx* ctx, fr_frame_timing* timing);  /* JFA -> SI -> PPI -> AT only */
 int fr_synchronize(fr_ctx* ctx);
@@ -266,6 +275,10 @@ int fr_set_shard_ex(fr_ctx* ctx, int rank, int count, int tile, int first_tracer
 int fr_shard_pack_active(fr_ctx* ctx, void* device_slab, size_t slab_bytes, uint32_t capacity, uint32_t* count);
 int fr_shard_unpack_active(fr_ctx* ctx, const void* device_slab, size_t slab_bytes, uint32_t capacity,
                            uint32_t count);
+/* fr_shard_unpack_active without the synchronisation: enqueued on the context stream after the work
+ * already there (the slab must stay valid until that work has run, e.g. until fr_synchronize). */
+int fr_shard_unpack_active_enqueue(fr_ctx* ctx, const void* device_slab, size_t slab_bytes, uint32_t capacity,
+                                   uint32_t count);
 int fr_shard_texels(fr_ctx* ctx, size_t* texels);
 int fr_shard_pack(fr_ctx* ctx, int buffer_id, void* device_slab, size_t bytes);
 int fr_shard_unpack(fr_ctx* ctx, int buffer_id, int src_rank, const void* device_slab, size_t bytes);

@@ -1,17 +1,22 @@
 #!/usr/bin/env python3
-"""Strong-scaling model of a tile-sharded view (BASELINE configs[3]/[4]) from one-GPU measurements.
+"""Strong-scaling model of one 4K view tile-sharded over G ranks by fr_group (BASELINE configs[2]-[4]),
+from one-GPU measurements of every rank's role.
 
-A G-rank view with fr_set_shard_ex(first_tracer = 1): ranks 1..G-1 trace the screen tiles round robin, rank 0
-computes the G-buffer and sampling (both needed by the reconstruction) and runs the reconstruction half on
-the gathered SHADING. On one GPU this measures, per G, the work of one tracing rank (its whole trace half,
-timed frames, median) and of the compositing rank (its front stages + the reconstruction half), plus the
-slab each tracer sends: its traced pixels, 20 B each (the sparse gather, bench.py's default for a static
-camera; the tile slabs of SHADING are reported beside it). The gather over xGMI is not measured here (one GPU): it is priced at an assumed
-link rate (each tracer has its own link to the root). Prints one JSON line per G.
+fr_group's roles in a view of G ranks (include/fovrt.h): view rank 0 runs JumpFlooding -> Sibson, view
+rank 1 pull-push -> A-Trous, and the screen tiles are dealt over all ranks by water filling on those
+reconstruction loads (fr_group_config.recon_cost, the same rule as group.cpp). Every rank runs the front
+stages and traces its tiles. On one GPU this script runs each distinct role's work as that rank would:
+a context warmed up on whole frames (so its carried history holds the view's seeds, as the gathered pixels
+keep it in the group), then switched to the role's tiles and chains, and K pipelined frames timed back to
+back (trace half + its reconstruction chain). The frame rate of the view is the slowest role's (the ranks
+pipeline against each other; the traced pixels, 20 B each, travel on the comm streams beside compute:
+their xGMI time is printed, priced at an assumed link rate, and not on the throughput path unless it
+exceeds a rank's frame). Prints one JSON line per G.
   python scripts/shard_model.py [scene=bunny|vokselia] [xgmi_GBs=64]"""
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -20,49 +25,108 @@ sys.path.insert(0, os.path.join(ROOT, "foveated-rendering-using-ray-tracing_amd"
 import torch  # noqa: E402,F401
 import fovrt  # noqa: E402
 
+RECON_COST = (0.5, 0.17)
+
+
+def level_weights(cost):
+    """group.cpp level_weights: trace shares s_r = max(0, lambda - c_r), sum 1."""
+    c = sorted(cost)
+    acc = 0.0
+    lam = 0.0
+    for k in range(1, len(c) + 1):
+        acc += c[k - 1]
+        lam = (1.0 + acc) / k
+        if k == len(c) or lam <= c[k]:
+            break
+    return [max(0.0, lam - x) for x in cost]
+
 
 def main():
+    import torch
     scene_name = sys.argv[1] if len(sys.argv) > 1 else "bunny"
     link = float(sys.argv[2]) if len(sys.argv) > 2 else 64.0
-    W, H = 3840, 2160
+    W, H, T, K = 3840, 2160, 128, 12
     vok = scene_name == "vokselia"
     scene = fovrt.SCENES[scene_name]
     cfg = dict(width=W, height=H, scene=scene, mask_mode=fovrt.MASK_SALIENCY if vok else fovrt.MASK_LOGPOLAR_SIGNED,
                spp=8 if vok else 4, diffuse_max_depth=3)
-    K = 7
+    cam = fovrt.Camera.preset(scene, W, H)
     t = fovrt.PathTracer(fovrt.Config(**cfg))
     t.initialize()
-    t.update_optix_variables(fovrt.Camera.preset(scene, W, H))
+    t.update_optix_variables(cam)
+    # the pixels a reconstruction rank receives from the others: every traced pixel of the frame, packed by a
+    # context that owns all tiles (rank 1 of 2, rank 0 empty), 20 B each
+    src = fovrt.PathTracer(fovrt.Config(**cfg))
+    src.initialize()
+    src.update_optix_variables(cam)
+    nt = ((W + T - 1) // T) * ((H + T - 1) // T)
+    src.set_shard_plan(1, 2, T, np.ones(nt, np.uint8))
+    for _ in range(3):
+        src.trace_frame(timing=False)
+    src.synchronize()
+    n_all = src.ray_count()
+    slab = torch.empty(n_all * 5, dtype=torch.float32, device="cuda")
+    assert src.shard_pack_active(slab.data_ptr(), n_all) == n_all
+    src.destroy()
 
-    def med(f, key="total_ms"):
-        v = []
-        for _ in range(K):
-            v.append(f()[key])
-        return float(np.median(v[2:]))
+    def pipelined(role_recon, n=K):
+        def one():
+            if role_recon is None:
+                t.frame(timing=False)
+                return
+            t.trace_frame(timing=False)
+            if role_recon:
+                t.shard_unpack_active_enqueue(slab.data_ptr(), n_all, n_all)
+                t.reconstruct_frame(timing=False)
+        for _ in range(3):
+            one()
+        t.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            one()
+        t.synchronize()
+        return (time.perf_counter() - t0) / n * 1e3
 
-    # the compositing rank reconstructs the gathered SHADING of the whole view: its cost does not depend
-    # on G, so it is measured on a complete frame (its own SHADING after a no-tile trace half would hold
-    # only carried history, without the sky's fresh samples: a different, much sparser seed set)
-    t.set_shard(0, 1, 128, 0)
-    full = med(lambda: t.frame(timing=True))
-    recon = med(lambda: t.reconstruct_frame(timing=True))
-    print(json.dumps({"G": 1, "scene": scene_name, "frame_ms": round(full, 4), "fps": round(1e3 / full, 1),
-                      "recon_ms": round(recon, 4)}))
+    t.set_shard_plan(0, 1, T, np.zeros(1, np.uint8))
+    t.set_recon_chains(3)
+    one = pipelined(None)
+    print(json.dumps({"G": 1, "scene": scene_name, "pipelined_frame_ms": round(one, 4), "fps": round(1e3 / one, 1),
+                      "pixels_received_by_recon_ranks": n_all}), flush=True)
     for G in (2, 4, 8):
-        t.set_shard(1, G, 128, 1)  # one tracing rank
-        tr = med(lambda: t.trace_frame(timing=True))
-        dense = t.shard_texels() * 16
-        slab = t.ray_count() * 20  # the sparse gather (fr_shard_pack_active): the traced pixels only
-        t.set_shard(0, G, 128, 1)  # the compositing rank: front stages (G-buffer, sampling), no tiles
-        front = med(lambda: t.trace_frame(timing=True))
-        gather = slab / (link * 1e9) * 1e3
-        # ranks overlap across frames: tracers trace frame N+1 while the root reconstructs frame N
-        frame = max(tr + gather, front + gather + recon)
-        print(json.dumps({"G": G, "scene": scene_name, "tracer_trace_ms": round(tr, 4), "root_front_ms": round(front, 4),
-                          "root_recon_ms": round(recon, 4), "slab_MB_per_tracer": round(slab / 1e6, 2),
-                          "dense_slab_MB_per_tracer": round(dense / 1e6, 1),
-                          "gather_ms_at_%gGBs" % link: round(gather, 4), "model_frame_ms": round(frame, 4),
-                          "model_fps": round(1e3 / frame, 1)}))
+        cost = [RECON_COST[0] if r == 0 else RECON_COST[1] if r == 1 else 0.0 for r in range(G)]
+        w = level_weights(cost)
+        owner = fovrt.shard_plan(W, H, T, G, w)
+        tiles = np.bincount(owner, minlength=G)
+        roles = {0: 1, 1: 2}
+        tracer = max(range(2, G), key=lambda r: tiles[r]) if G > 2 else None
+        if tracer is not None:
+            roles[tracer] = 0
+        res = {}
+        for r, chains in roles.items():
+            t.set_shard_plan(r, G, T, owner)
+            t.set_recon_chains(max(chains, 1))
+            for form in (1, 2):
+                t.set_sample_sum(form)
+                ms = pipelined(chains != 0)
+                res.setdefault(r, {"chains": chains, "tiles": int(tiles[r])})["pipelined_frame_ms_form%d" % form] = round(ms, 4)
+            t.set_sample_sum(1)
+            st = t.trace_frame(timing=True)
+            res[r].update({"active_px": int(st["ray_count"]),
+                           "trace_ms": round(st["geometry_ms"] + st["sampling_ms"] + st["optimize_ms"] + st["shading_ms"], 4),
+                           "megakernel_ms": round(st["shade_paths_ms"], 4)})
+            if chains:
+                rt = t.reconstruct_frame(timing=True)
+                res[r]["recon_ms"] = round(rt["jfa_ms"] + rt["sibson_ms"] + rt["pullpush_ms"] + rt["atrous_ms"], 4)
+        out = {"G": G, "scene": scene_name, "weights": [round(x, 3) for x in w], "tiles": tiles.tolist(), "roles": res}
+        for form in (1, 2):
+            frame = max(v["pipelined_frame_ms_form%d" % form] for v in res.values())
+            out["model_frame_ms_form%d" % form] = round(frame, 4)
+            out["model_fps_form%d" % form] = round(1e3 / frame, 1)
+            out["speedup_form%d" % form] = round(one / frame, 3)
+        send = max(v["active_px"] for v in res.values()) * 20
+        out["max_send_MB"] = round(send / 1e6, 2)
+        out["xgmi_ms_at_%gGBs" % link] = round(send / (link * 1e9) * 1e3, 4)
+        print(json.dumps(out), flush=True)
     t.destroy()
 
 
