@@ -734,8 +734,11 @@ static int resolve(fr_ctx* c, int id, int* phys) {
 static int enqueue_jfa(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {
   int p;
   if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "jfa: bad input buffer");
+  const bool run_form = c->cfg.sibson_mode == 0;
   launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->ftab, c->W, c->H,
+             run_form ? c->sib_prefix : nullptr, run_form ? c->sib_blocks : nullptr,
              stream ? stream : c->stream);
+  c->sib_prefix_fresh = run_form;
   return check_launch(c);
 }
 static int enqueue_sibson(fr_ctx* c, hipStream_t stream = nullptr) {
@@ -743,7 +746,7 @@ static int enqueue_sibson(fr_ctx* c, hipStream_t stream = nullptr) {
     launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, stream ? stream : c->stream);
   else  // run form (default): exact tap sets, rounding-level differences
     launch_sibson_runs(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->sib_prefix, c->sib_blocks, c->img[P_SIBSON], c->W,
-                       c->H, stream ? stream : c->stream);
+                       c->H, c->sib_prefix_fresh, stream ? stream : c->stream);
   return check_launch(c);
 }
 static int enqueue_pullpush(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {
@@ -1223,6 +1226,7 @@ int fr_write_buffer(fr_ctx* c, int id, const void* host, size_t bytes) {
   if (!host || bytes > v.bytes) return fail(c, FR_E_INVALID, "write_buffer: size");
   HIP_TRY(c, hipMemcpyAsync(v.device_ptr, host, bytes, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (id == FR_BUF_JFA_COLOR) c->sib_prefix_fresh = false;  // Sibson's row prefix sums no longer match it
   if (id == FR_BUF_MASK) {
     // a host-written mask must also drive the compaction: rebuild the wave ballots from it
     c->compacted = false;

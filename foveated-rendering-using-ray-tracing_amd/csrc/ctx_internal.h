@@ -39,9 +39,9 @@ void launch_composite(const f4*, int, int, int, f4*, hipStream_t);
 void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
 void launch_shard_pack_active(const uint32_t*, const uint32_t*, uint32_t, const f4*, f4*, uint32_t*, hipStream_t);
 void launch_shard_unpack_active(const f4*, const uint32_t*, uint32_t, uint32_t, f4*, f4*, hipStream_t);
-void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, hipStream_t);
+void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, f4*, f4*, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
-void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, int, int, hipStream_t);
+void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, int, int, bool, hipStream_t);
 int sibson_prefix_blocks(int W);
 struct BvhWork;
 bool gpu_build_bvh(BvhWork**, const f3*, int, BvhNode*, TriGeo*, int32_t*, int*, int*, int*, hipStream_t, std::string&);
@@ -180,6 +180,7 @@ struct fr_ctx {
   float* ftab = nullptr;  // texel-centre coordinates ((x + 0.5) / W, x < W; then (y + 0.5) / H)
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
   f4 *sib_prefix = nullptr, *sib_blocks = nullptr;  // Sibson run form: per-row block prefix sums + block totals
+  bool sib_prefix_fresh = false;  // the last JFA wrote them with JFA_COLOR (cleared when JFA_COLOR is written)
   int pp_S = 0;
   DevStats* stats = nullptr;
   FrameUniforms U;

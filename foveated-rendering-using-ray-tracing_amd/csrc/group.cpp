@@ -301,6 +301,7 @@ int fr_group_config_default(fr_group_config* cfg) {
   cfg->split_recon = 1;
   cfg->recon_cost[0] = 0.5f;
   cfg->recon_cost[1] = 0.17f;
+  cfg->sample_sum = 2;
   return FR_OK;
 }
 
@@ -360,6 +361,7 @@ int fr_group_create(fr_ctx* const* ctxs, int n, void* rccl_comm, const fr_group_
   const int G = R / cfg.views;
   if (G > FR_GROUP_MAX_VIEW_RANKS) return gfail(FR_E_UNSUPPORTED, "fr_group_create: more than 16 ranks per view");
   if (cfg.tile < 16 || cfg.tile % 16 || cfg.tile > 4096) return gfail(FR_E_INVALID, "fr_group_create: tile must be a multiple of 16");
+  if (cfg.sample_sum < -1 || cfg.sample_sum > 2) return gfail(FR_E_INVALID, "fr_group_create: sample_sum is -1, 0, 1 or 2");
   for (int i = 0; i < n; i++)
     if (!ctxs[i] || ctxs[i]->W != ctxs[0]->W || ctxs[i]->H != ctxs[0]->H || ctxs[i]->cfg.spp != ctxs[0]->cfg.spp)
       return gfail(FR_E_INVALID, "fr_group_create: every context needs the same width, height and spp");
@@ -410,6 +412,8 @@ int fr_group_create(fr_ctx* const* ctxs, int n, void* rccl_comm, const fr_group_
       return bail(gfail(rc, std::string("fr_group_create: ") + fr_last_error(c)));
     }
     c->recon_chains = L.chains;
+    if (G > 1 && cfg.sample_sum >= 0)
+      if (int rc = fr_set_sample_sum(c, cfg.sample_sum)) return bail(gfail(rc, std::string("fr_group_create: ") + fr_last_error(c)));
     if (hipStreamCreateWithFlags(&L.comm, hipStreamNonBlocking) != hipSuccess) return bail(gfail(FR_E_HIP, "group: stream"));
     hipEventCreateWithFlags(&L.ev_packed, hipEventDisableTiming);
     hipEventCreateWithFlags(&L.ev_out, hipEventDisableTiming);

@@ -93,7 +93,8 @@ class fr_stage_times(C.Structure):
 
 class fr_group_config(C.Structure):
     _fields_ = [("views", C.c_int), ("tile", C.c_int), ("split_recon", C.c_int), ("moving_camera", C.c_int),
-                ("composite", C.c_int), ("recon_cost", C.c_float * 2), ("weights", C.c_float * GROUP_MAX_VIEW_RANKS)]
+                ("composite", C.c_int), ("recon_cost", C.c_float * 2), ("weights", C.c_float * GROUP_MAX_VIEW_RANKS),
+                ("sample_sum", C.c_int)]
 
 
 class fr_scene_arrays(C.Structure):
@@ -727,7 +728,7 @@ class Group:
     nranks, rank) makes this process's tracer one rank of an RCCL communicator."""
 
     def __init__(self, tracers, views=1, tile=128, split_recon=True, moving_camera=False, composite=False,
-                 recon_cost=None, weights=None, _comm=None):
+                 recon_cost=None, weights=None, sample_sum=None, _comm=None):
         lib = load_library()
         cfg = fr_group_config()
         lib.fr_group_config_default(C.byref(cfg))
@@ -738,6 +739,8 @@ class Group:
         if weights is not None:
             for i, w in enumerate(weights):
                 cfg.weights[i] = float(w)
+        if sample_sum is not None:
+            cfg.sample_sum = int(sample_sum)
         self.tracers = list(tracers)
         arr = (C.c_void_p * len(self.tracers))(*[t._ctx.value for t in self.tracers])
         h = C.c_void_p()

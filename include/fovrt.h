@@ -313,6 +313,9 @@ typedef struct fr_group_config {
                               trace work (default 0.5, 0.17: JFA + Sibson, pull-push + A-Trous at 4K);
                               the tiles are dealt so that every rank's total is level (water filling) */
   float weights[FR_GROUP_MAX_VIEW_RANKS];  /* explicit tracing weights per view rank; all 0 = from recon_cost */
+  int sample_sum;          /* fr_set_sample_sum on every rank when G >= 2 (default 2: fixed point with the tail
+                              handoff, which shortens a tracer's small launch; the view then equals a one-GPU
+                              frame in that form); -1 leaves the contexts as they are */
 } fr_group_config;
 int fr_group_config_default(fr_group_config* cfg);
 /* RCCL bootstrap for callers without their own: rank 0 creates the 128-byte unique id, every rank

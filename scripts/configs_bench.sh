@@ -12,5 +12,7 @@ run() {
 run C1 --scene box --width 512 --height 512 --spp 1 --dmd 1 --mask uniform
 run C2 --scene bunny --width 1920 --height 1080 --spp 4 --dmd 1 --mask logpolar10
 run C3 --no-cpu-baseline
+# C3 with an eye-tracked gaze: a scripted cursor path every frame (the log-polar mask recomputed each frame)
+run C3gaze --no-cpu-baseline --gaze-path
 run C4 --no-cpu-baseline --scene vokselia --spp 8 --dmd 1 --mask saliency
 run C5 --no-cpu-baseline --scene vokselia --spp 8 --dmd 3 --mask saliency

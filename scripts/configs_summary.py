@@ -4,7 +4,7 @@ import glob, json, re, sys
 
 out = []
 for f in sorted(glob.glob("gpurun_out/cfg_C*.log")):
-    name = re.search(r"cfg_(C\d)", f).group(1)
+    name = re.search(r"cfg_(C\d\w*)\.log", f).group(1)
     lines = [l for l in open(f) if l.startswith("{")]
     if not lines:
         continue
@@ -14,7 +14,7 @@ for f in sorted(glob.glob("gpurun_out/cfg_C*.log")):
            "diffuse_max_depth": c["diffuse_max_depth"], "mask_mode": c["mask_mode"],
            "foveal_density": c["foveal_density"], "Mrays_s": d["value"], "fps": d["fps"],
            "ms_per_step": d["ms_per_step"], "stages_ms": {k: v["ms"] for k, v in d["stages"].items()},
-           "megakernel_ms": d["roofline"].get("megakernel_ms")}
+           "megakernel_ms": d["roofline"].get("megakernel_ms"), "gaze": c.get("gaze")}
     if "cpu_baseline" in d:
         row["cpu_baseline"] = {k: d["cpu_baseline"][k] for k in ("value", "unit", "cores", "kind", "fps")}
     out.append(row)

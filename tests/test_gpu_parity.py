@@ -786,6 +786,9 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
     mk = lambda: make_tracer(fovrt_mod, W, H, scene=1, mask=mask, spp=4, dmd=3)
     ranks = [mk() for _ in range(R)]
     fulls = [mk() for _ in range(V)]
+    if G > 1:  # the group sums samples in fixed point (fr_group_config.sample_sum 2): the references too
+        for f in fulls:
+            f.set_sample_sum(2)
     cams = []
     for v in range(V):
         cam = fovrt_mod.Camera.preset(1, W, H)
