@@ -494,6 +494,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   U.sqrt_spp = (int)floor(sqrt((double)cfg.spp) + 1e-9);
   U.mask_mode = cfg.mask_mode;
   U.shard_rank = 0; U.shard_count = 1; U.shard_tile = 128; U.shard_tiles_x = (c->W + 127) / 128; U.shard_map = nullptr;
+  U.front_need = nullptr; U.front_pixels = 0;
   {
     fr_camera_pose pose;
     float eye[3], tgt[3], upv[3] = {0, 1, 0};
@@ -528,7 +529,7 @@ int fr_destroy(fr_ctx* c) {
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
   for (int k = 0; k < fr_ctx::MAX_SLOTS; k++) { fr(c->mask_p[k]); fr(c->ray_count_p[k]); fr(c->active_p[k]); fr(c->owner_counts_p[k]); }
-  fr(c->bcount); fr(c->shard_map);
+  fr(c->bcount); fr(c->shard_map); fr(c->front_need);
   if (c->h_counts) hipHostFree(c->h_counts);
   for (auto e : c->ev_counts) if (e) hipEventDestroy(e);
   fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->item_store); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
@@ -621,6 +622,12 @@ static int enqueue_geometry(fr_ctx* c, hipStream_t fs) {
     const size_t bytes = (size_t)c->W * c->H * sizeof(f4);
     hipMemsetAsync(c->img[c->hist_cur], 0, bytes, c->stream);
     hipMemsetAsync(c->img[c->hist_cache], 0, bytes, c->stream);
+  }
+  if (c->front_local) {  // the primaries this G-buffer traces: the needed tiles and the gaze pixel's
+    const int t8 = gaze_tile8(c->U);
+    const int tx8 = (c->W + 7) / 8;
+    const uint32_t gw = (uint32_t)std::min(8, c->W - (t8 % tx8) * 8), gh = (uint32_t)std::min(8, c->H - (t8 / tx8) * 8);
+    c->U.front_pixels = c->front_need_px + (c->front_need_h[t8] ? 0u : gw * gh);
   }
   launch_gbuffer(c->dsc, c->U, c->img[P_pos(c)], c->img[P_nrm(c)], c->img[c->depth_cur], c->img[P_DIFFUSE],
                  c->img[P_wgt(c)], c->gclass, c->stats, fs);
@@ -1032,6 +1039,8 @@ int fr_shard_plan(int W, int H, int tile, int count, const float* weights, uint8
   return FR_OK;
 }
 
+static int update_front_need(fr_ctx* c);
+
 int fr_set_shard_plan(fr_ctx* c, int rank, int count, int tile, const uint8_t* owner, size_t ntiles) {
   if (!c) return FR_E_INVALID;
   if (count < 1 || count > FR_MAX_SHARD_RANKS || rank < 0 || rank >= count || tile < 16 || tile % 16 || tile > 4096)
@@ -1064,7 +1073,53 @@ int fr_set_shard_plan(fr_ctx* c, int rank, int count, int tile, const uint8_t* o
   c->U.shard_tiles_x = tx;
   c->U.shard_map = c->shard_map;
   c->compacted = false;
+  if (count == 1) c->front_local = false;
+  return update_front_need(c);
+}
+
+// The 8x8 tiles a tile-local front computes: an owned 16x16 block's saliency cells (origins 4 px apart)
+// read taps 4 px beyond their origin, so block b's stencil covers pixels [16b - 4, 16b + 16] on each
+// axis. The left half of block k is read by blocks k-1 and k, the right half by k and k+1.
+static int update_front_need(fr_ctx* c) {
+  if (!c->front_local) {
+    c->U.front_need = nullptr;
+    return FR_OK;
+  }
+  const int tx8 = (c->W + 7) / 8, ty8 = (c->H + 7) / 8;
+  const int bx = (c->W + 15) / 16, by = (c->H + 15) / 16;
+  const int T = c->U.shard_tile;
+  auto owned = [&](int X, int Y) {
+    if (X < 0 || Y < 0 || X >= bx || Y >= by) return false;
+    return c->shard_owner[(size_t)((Y * 16) / T) * c->U.shard_tiles_x + (X * 16) / T] == c->U.shard_rank;
+  };
+  c->front_need_h.assign((size_t)tx8 * ty8, 0);
+  c->front_need_px = 0;
+  for (int j = 0; j < ty8; j++)
+    for (int i = 0; i < tx8; i++) {
+      const int X = i >> 1, Y = j >> 1, dx = (i & 1) ? 1 : -1, dy = (j & 1) ? 1 : -1;
+      const bool need = owned(X, Y) || owned(X + dx, Y) || owned(X, Y + dy) || owned(X + dx, Y + dy);
+      if (!need) continue;
+      c->front_need_h[(size_t)j * tx8 + i] = 1;
+      c->front_need_px += (uint32_t)(std::min(8, c->W - i * 8) * std::min(8, c->H - j * 8));
+    }
+  if (!c->front_need) HIP_TRY(c, hipMalloc((void**)&c->front_need, c->front_need_h.size()));
+  HIP_TRY(c, hipMemcpy(c->front_need, c->front_need_h.data(), c->front_need_h.size(), hipMemcpyHostToDevice));
+  c->U.front_need = c->front_need;
   return FR_OK;
+}
+
+int fr_set_front_local(fr_ctx* c, int on) {
+  if (!c) return FR_E_INVALID;
+  if (on != 0 && on != 1) return fail(c, FR_E_INVALID, "fr_set_front_local: on is 0 or 1");
+  if (on && c->U.shard_count <= 1) return fail(c, FR_E_STATE, "fr_set_front_local: needs a shard plan with count > 1");
+  if ((bool)on == c->front_local) return FR_OK;
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream5));
+  c->front_local = on != 0;
+  c->compacted = false;
+  return update_front_need(c);
 }
 
 int fr_set_shard_ex(fr_ctx* c, int rank, int count, int tile, int first_tracer) {

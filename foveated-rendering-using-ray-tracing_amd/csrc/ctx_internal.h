@@ -127,9 +127,15 @@ struct fr_ctx {
   uint32_t* owner_counts_p[MAX_SLOTS] = {};
   uint32_t* h_counts = nullptr;  // MAX_SLOTS x FR_MAX_SHARD_RANKS, pinned
   hipEvent_t ev_counts[MAX_SLOTS] = {};
-  int recon_chains = 3;
+  // Tile-local front stages (fr_set_front_local): per 8x8 pixel tile, does this rank's sampling read
+  // it (front_need, device; FrameUniforms::front_need while on); front_need_px = their pixel count.
+  bool front_local = false;
+  uint8_t* front_need = nullptr;
+  std::vector<uint8_t> front_need_h;
+  uint32_t front_need_px = 0;
+  int recon_chains = 3;             // reconstruction chains this context runs: 1 JFA -> Sibson, 2 pull-push -> A-Trous
   hipEvent_t recon_gate = nullptr;  // when set, chain 2 (pull-push -> A-Trous) waits for it (a group's
-                                    // composite reads the last A-Trous image)  // reconstruction chains this context runs: 1 JFA -> Sibson, 2 pull-push -> A-Trous
+                                    // composite reads the last A-Trous image)
   uint8_t* mask_p[MAX_SLOTS] = {};
   uint32_t* active_p[MAX_SLOTS] = {};
   uint32_t* ray_count_p[MAX_SLOTS] = {};

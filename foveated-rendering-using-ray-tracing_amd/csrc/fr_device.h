@@ -104,7 +104,22 @@ struct FrameUniforms {
   // in a packed tile slab); shard_count 1 = the whole screen (shard_map unused)
   int32_t shard_rank, shard_count, shard_tile, shard_tiles_x;
   const uint32_t* shard_map;
+  // tile-local front stages (fr_set_front_local, a tracing rank of a static-camera group): the G-buffer
+  // runs on the 8x8 pixel tiles with front_need[t] != 0 (this rank's tiles plus the saliency stencil's
+  // halo) and on the gaze pixel's tile; k_sampling and the carry only on this rank's tiles. front_pixels
+  // = the G-buffer pixels that traces (the primary-ray count). Null = the whole screen.
+  const uint8_t* front_need;
+  uint32_t front_pixels;
 };
+
+// The 8x8 tile of the gaze pixel (its depth sets the saliency focus in k_sampling; the clamp is
+// k_sampling's).
+FR_HD int gaze_tile8(const FrameUniforms& U) {
+  uint32_t gx = f2u_sat(U.gaze.x), gy = f2u_sat(U.gaze.y);
+  gx = gx < (uint32_t)U.width - 1 ? gx : (uint32_t)U.width - 1;
+  gy = gy < (uint32_t)U.height - 1 ? gy : (uint32_t)U.height - 1;
+  return (int)((gy >> 3) * (uint32_t)((U.width + 7) >> 3) + (gx >> 3));
+}
 
 // XCD-aware block order: blocks b, b+8, b+16, ... share an XCD (and its L2), so hand each of the 8
 // such classes one contiguous run of tiles (row-major bands of the image) instead of every 8th tile.

@@ -55,6 +55,7 @@ struct fr_group {
   fr_group_config cfg;
   std::vector<uint8_t> owner;       // tile -> view rank (the same plan in every view)
   std::vector<int> tiles_per_vrank;
+  int jfa_ranks = 1;                // view ranks taking JFA -> Sibson in turns (fr_group_config.jfa_ranks)
   uint64_t frame = 0;
   bool composite_done = false;
 };
@@ -63,12 +64,20 @@ namespace {
 
 int view_of(const fr_group* g, int rank) { return rank / g->G; }
 int rank_of(const fr_group* g, int view, int vrank) { return view * g->G + vrank; }
+// The view ranks that take JumpFlooding -> Sibson in turns (one frame each): view rank 0, then 2, 3, ...
+// (view rank 1 runs pull-push -> A-Trous, whose push atlas carries state from frame to frame).
+bool runs_jfa(const fr_group* g, int vrank) { return vrank == 0 || (vrank >= 2 && vrank <= g->jfa_ranks); }
 int chains_of(const fr_group* g, int vrank) {
   if (g->G == 1) return 3;
   const bool split = g->cfg.split_recon != 0;
   if (vrank == 0) return split ? 1 : 3;
   if (vrank == 1 && split) return 2;
-  return 0;
+  return runs_jfa(g, vrank) ? 1 : 0;
+}
+// The view rank whose turn it is to run JumpFlooding -> Sibson on frame f.
+int jfa_turn(const fr_group* g, uint64_t f) {
+  const int k = (int)(f % (uint64_t)g->jfa_ranks);
+  return k == 0 ? 0 : k + 1;
 }
 // The view rank whose A-Trous image is the view's output (the composite's source).
 int output_vrank(const fr_group* g) { return g->G >= 2 && g->cfg.split_recon ? 1 : 0; }
@@ -302,6 +311,8 @@ int fr_group_config_default(fr_group_config* cfg) {
   cfg->recon_cost[0] = 0.5f;
   cfg->recon_cost[1] = 0.17f;
   cfg->sample_sum = 2;
+  cfg->front_local = 1;
+  cfg->jfa_ranks = 0;
   return FR_OK;
 }
 
@@ -370,6 +381,11 @@ int fr_group_create(fr_ctx* const* ctxs, int n, void* rccl_comm, const fr_group_
   g->R = R; g->V = cfg.views; g->G = G;
   g->W = ctxs[0]->W; g->H = ctxs[0]->H;
   g->comm = (ncclComm_t)rccl_comm;
+  if (cfg.jfa_ranks < 0 || cfg.jfa_ranks > 1 + std::max(0, G - 2) || (cfg.jfa_ranks > 1 && !cfg.split_recon)) {
+    delete g;
+    return gfail(FR_E_INVALID, "fr_group_create: jfa_ranks is 0 (auto) or 1 .. G - 1, and above 1 only with split_recon");
+  }
+  g->jfa_ranks = cfg.jfa_ranks ? cfg.jfa_ranks : (cfg.split_recon && G >= 6 ? 2 : 1);
   auto bail = [&](int rc) { fr_group_destroy(g); return rc; };
   // the tile plan (the same in every view)
   const int T = cfg.tile;
@@ -385,9 +401,14 @@ int fr_group_create(fr_ctx* const* ctxs, int n, void* rccl_comm, const fr_group_
       std::vector<double> cost(G, 0.0);
       for (int r = 0; r < G; r++) {
         const int ch = chains_of(g, r);
-        cost[r] = ((ch & 1) ? cfg.recon_cost[0] : 0.0) + ((ch & 2) ? cfg.recon_cost[1] : 0.0);
+        cost[r] = ((ch & 1) ? cfg.recon_cost[0] / g->jfa_ranks : 0.0) + ((ch & 2) ? cfg.recon_cost[1] : 0.0);
       }
       level_weights(cost, w);
+      // a rank left with a sliver of the tiles would still pay a whole launch's critical path (the
+      // longest refraction trees of a dense foveal tile take ~2 ms however few tiles there are), on top
+      // of its reconstruction chain: slivers below a fifth of the largest share go to the others
+      const float wmax = *std::max_element(w.begin(), w.end());
+      for (float& x : w) if (x < 0.2f * wmax) x = 0.0f;
     }
     g->owner.resize(ntiles);
     if (int rc = fr_shard_plan(g->W, g->H, T, G, w.data(), g->owner.data(), ntiles))
@@ -414,6 +435,9 @@ int fr_group_create(fr_ctx* const* ctxs, int n, void* rccl_comm, const fr_group_
     c->recon_chains = L.chains;
     if (G > 1 && cfg.sample_sum >= 0)
       if (int rc = fr_set_sample_sum(c, cfg.sample_sum)) return bail(gfail(rc, std::string("fr_group_create: ") + fr_last_error(c)));
+    // a tracer of a still camera needs the front stages of its own tiles only (it receives nothing)
+    if (G > 1 && L.chains == 0 && cfg.front_local && !cfg.moving_camera)
+      if (int rc = fr_set_front_local(c, 1)) return bail(gfail(rc, std::string("fr_group_create: ") + fr_last_error(c)));
     if (hipStreamCreateWithFlags(&L.comm, hipStreamNonBlocking) != hipSuccess) return bail(gfail(FR_E_HIP, "group: stream"));
     hipEventCreateWithFlags(&L.ev_packed, hipEventDisableTiming);
     hipEventCreateWithFlags(&L.ev_out, hipEventDisableTiming);
@@ -458,10 +482,13 @@ int fr_group_frame(fr_group* g, fr_frame_timing* t) {
   if (g->G > 1)
     if (int rc = exchange(g)) return rc;
   // 3. the reconstruction chains of this frame on their ranks
+  const int turn = jfa_turn(g, g->frame);
   for (int i = 0; i < n; i++) {
     GroupRank& L = g->loc[i];
-    if (!L.chains) continue;
+    const int run = g->G > 1 && L.vrank != turn ? (L.chains & ~1) : L.chains;
+    if (!run) continue;
     hipSetDevice(L.c->cfg.device);
+    L.c->recon_chains = run;
     fr_frame_timing rt{};
     if (int rc = fri::frame_half(L.c, t ? &rt : nullptr, false, true))
       return gfail(rc, std::string("group reconstruction: ") + fr_last_error(L.c));
@@ -520,6 +547,23 @@ int fr_group_rank_info(fr_group* g, int i, int* view, int* view_rank, int* chain
   if (view_rank) *view_rank = L.vrank;
   if (chains) *chains = L.chains;
   if (tiles) *tiles = L.tiles;
+  return FR_OK;
+}
+
+int fr_group_output_ranks(fr_group* g, int view, int* jfa_rank, int* atrous_rank) {
+  if (!g || view < 0 || view >= g->V) return FR_E_INVALID;
+  if (!g->frame) return gfail(FR_E_STATE, "fr_group_output_ranks: no frame yet");
+  if (jfa_rank) *jfa_rank = rank_of(g, view, g->G > 1 ? jfa_turn(g, g->frame - 1) : 0);
+  if (atrous_rank) *atrous_rank = rank_of(g, view, output_vrank(g));
+  return FR_OK;
+}
+
+int fr_group_tile_owners(fr_group* g, uint8_t* owner, size_t ntiles) {
+  if (!g || !owner) return FR_E_INVALID;
+  const int T = g->cfg.tile;
+  const size_t nt = (size_t)((g->W + T - 1) / T) * ((g->H + T - 1) / T);
+  if (ntiles != nt) return gfail(FR_E_INVALID, "fr_group_tile_owners: ntiles != ceil(W/tile) * ceil(H/tile)");
+  for (size_t t = 0; t < nt; t++) owner[t] = g->G > 1 ? g->owner[t] : 0;
   return FR_OK;
 }
 

@@ -94,7 +94,8 @@ class fr_stage_times(C.Structure):
 class fr_group_config(C.Structure):
     _fields_ = [("views", C.c_int), ("tile", C.c_int), ("split_recon", C.c_int), ("moving_camera", C.c_int),
                 ("composite", C.c_int), ("recon_cost", C.c_float * 2), ("weights", C.c_float * GROUP_MAX_VIEW_RANKS),
-                ("sample_sum", C.c_int)]
+                ("sample_sum", C.c_int), ("front_local", C.c_int),
+                ("jfa_ranks", C.c_int)]
 
 
 class fr_scene_arrays(C.Structure):
@@ -141,6 +142,7 @@ _SIGS = {
     "fr_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_set_recon_chains": [C.c_void_p, C.c_int],
     "fr_set_sample_sum": [C.c_void_p, C.c_int],
+    "fr_set_front_local": [C.c_void_p, C.c_int],
     "fr_shard_unpack_active_enqueue": [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32],
     "fr_trace_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_reconstruct_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
@@ -178,6 +180,8 @@ _SIGS = {
     "fr_group_composite": [C.c_void_p, C.c_void_p, C.c_size_t],
     "fr_group_rank_info": [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
                            C.POINTER(C.c_int)],
+    "fr_group_tile_owners": [C.c_void_p, C.c_void_p, C.c_size_t],
+    "fr_group_output_ranks": [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "fr_group_synchronize": [C.c_void_p],
     "fr_group_destroy": [C.c_void_p],
     "fr_group_last_error": [],
@@ -489,6 +493,10 @@ class PathTracer:
         self._check(_lib.fr_shard_unpack_active_enqueue(self._ctx, C.c_void_p(device_ptr), int(capacity) * 20,
                                                         int(capacity), int(count)))
 
+    def set_front_local(self, on=True):
+        """fr_set_front_local: front stages on this rank's tiles plus halo only (a still camera's tracer)."""
+        self._check(_lib.fr_set_front_local(self._ctx, int(bool(on))))
+
     def set_recon_chains(self, chains):
         """Reconstruction chains this context runs: bit 0 JFA -> Sibson, bit 1 pull-push -> A-Trous."""
         self._check(_lib.fr_set_recon_chains(self._ctx, int(chains)))
@@ -728,7 +736,8 @@ class Group:
     nranks, rank) makes this process's tracer one rank of an RCCL communicator."""
 
     def __init__(self, tracers, views=1, tile=128, split_recon=True, moving_camera=False, composite=False,
-                 recon_cost=None, weights=None, sample_sum=None, _comm=None):
+                 recon_cost=None, weights=None, sample_sum=None, front_local=None, jfa_ranks=None,
+                 _comm=None):
         lib = load_library()
         cfg = fr_group_config()
         lib.fr_group_config_default(C.byref(cfg))
@@ -741,6 +750,10 @@ class Group:
                 cfg.weights[i] = float(w)
         if sample_sum is not None:
             cfg.sample_sum = int(sample_sum)
+        if front_local is not None:
+            cfg.front_local = int(bool(front_local))
+        if jfa_ranks is not None:
+            cfg.jfa_ranks = int(jfa_ranks)
         self.tracers = list(tracers)
         arr = (C.c_void_p * len(self.tracers))(*[t._ctx.value for t in self.tracers])
         h = C.c_void_p()
@@ -788,6 +801,20 @@ class Group:
         v, vr, ch, tl = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         self._check(_lib.fr_group_rank_info(self._h, int(i), C.byref(v), C.byref(vr), C.byref(ch), C.byref(tl)))
         return {"view": v.value, "view_rank": vr.value, "chains": ch.value, "tiles": tl.value}
+
+    def output_ranks(self, view=0):
+        """fr_group_output_ranks: (rank holding the last frame's JFA / Sibson, rank holding its A-Trous)."""
+        a, b = C.c_int(), C.c_int()
+        self._check(_lib.fr_group_output_ranks(self._h, int(view), C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def tile_owners(self, width, height):
+        """fr_group_tile_owners: the view rank tracing each screen tile, as a (tiles_y, tiles_x) array."""
+        T = int(self.config.tile)
+        tx, ty = (width + T - 1) // T, (height + T - 1) // T
+        out = np.zeros(tx * ty, np.uint8)
+        self._check(_lib.fr_group_tile_owners(self._h, out.ctypes.data, out.size))
+        return out.reshape(ty, tx)
 
     def synchronize(self):
         self._check(_lib.fr_group_synchronize(self._h))

@@ -258,6 +258,14 @@ int fr_shard_plan(int width, int height, int tile, int count, const float* weigh
 /* Active pixels of every rank of the view in the last front stages (sampling + compaction), counted
  * on this rank from its own full mask: the pixels rank r traces and sends. Synchronises the front. */
 int fr_shard_counts(fr_ctx* ctx, uint32_t* counts, int n);
+/* Tile-local front stages for a tracing rank of a static camera (on = 1; needs count > 1 in the shard
+ * plan): the G-buffer runs only on this rank's tiles plus the 4-pixel halo the saliency stencil reads
+ * (and on the gaze pixel's 8x8 tile), and the sampling mask, compaction and the history carry only on
+ * this rank's tiles. Its traced pixels are unchanged; every other pixel of its buffers is unspecified,
+ * and fr_shard_counts reports 0 for the other ranks. The reprojection reads the previous frame at the
+ * same pixel only while the camera is still, so a moving camera needs on = 0 (the default). A new shard
+ * plan keeps the setting (and recomputes the tiles); a whole-screen plan turns it off. */
+int fr_set_front_local(fr_ctx* ctx, int on);
 /* The same with the tiles dealt over ranks first_tracer .. count-1 only (tile t to rank
  * first_tracer + t % (count - first_tracer)); ranks below first_tracer trace nothing. first_tracer = 1
  * leaves the view's compositing rank 0 to the G-buffer and the reconstruction half, which no other
@@ -316,6 +324,11 @@ typedef struct fr_group_config {
   int sample_sum;          /* fr_set_sample_sum on every rank when G >= 2 (default 2: fixed point with the tail
                               handoff, which shortens a tracer's small launch; the view then equals a one-GPU
                               frame in that form); -1 leaves the contexts as they are */
+  int front_local;         /* 1 (default): with a still camera, ranks that only trace run their front stages
+                              on their own tiles plus halo (fr_set_front_local); ignored with moving_camera */
+  int jfa_ranks;           /* view ranks that take JumpFlooding -> Sibson in turns, one frame each: view rank 0,
+                              then 2, 3, ... (they all receive every traced pixel; the chain keeps no state
+                              across frames). 0 (default) = auto: 2 when G >= 6 with split_recon, else 1 */
 } fr_group_config;
 int fr_group_config_default(fr_group_config* cfg);
 /* RCCL bootstrap for callers without their own: rank 0 creates the 128-byte unique id, every rank
@@ -335,6 +348,12 @@ int fr_group_composite(fr_group* g, void* out, size_t bytes);
 /* Roles of local rank i: *view, *view_rank, *chains (bit 0 JFA -> Sibson, bit 1 pull-push -> A-Trous
  * run here) and *tiles, the number of screen tiles it traces. */
 int fr_group_rank_info(fr_group* g, int i, int* view, int* view_rank, int* chains, int* tiles);
+/* Where the last frame's outputs of a view are: the global rank holding its JFA / Sibson images (the
+ * rank whose turn it was, see jfa_ranks) and the one holding its pull-push / A-Trous images. */
+int fr_group_output_ranks(fr_group* g, int view, int* jfa_rank, int* atrous_rank);
+/* The tile plan of the views: owner[t] = the view rank that traces tile t (ntiles = ceil(W/tile) *
+ * ceil(H/tile); all 0 when G = 1). */
+int fr_group_tile_owners(fr_group* g, uint8_t* owner, size_t ntiles);
 int fr_group_synchronize(fr_group* g);
 int fr_group_destroy(fr_group* g);  /* the contexts trace the whole screen again */
 const char* fr_group_last_error(void);  /* the failure of the calling thread's last fr_group_* / fr_rccl_* call */

@@ -5,7 +5,7 @@ from one-GPU measurements of every rank's role.
 fr_group's roles in a view of G ranks (include/fovrt.h): view rank 0 runs JumpFlooding -> Sibson, view
 rank 1 pull-push -> A-Trous, and the screen tiles are dealt over all ranks by water filling on those
 reconstruction loads (fr_group_config.recon_cost, the same rule as group.cpp). Every rank runs the front
-stages and traces its tiles. On one GPU this script runs each distinct role's work as that rank would:
+stages (a tracer on its own tiles plus halo only, fr_set_front_local) and traces its tiles. On one GPU this script runs each distinct role's work as that rank would:
 a context warmed up on whole frames (so its carried history holds the view's seeds, as the gathered pixels
 keep it in the group), then switched to the role's tiles and chains, and K pipelined frames timed back to
 back (trace half + its reconstruction chain). The frame rate of the view is the slowest role's (the ranks
@@ -29,7 +29,7 @@ RECON_COST = (0.5, 0.17)
 
 
 def level_weights(cost):
-    """group.cpp level_weights: trace shares s_r = max(0, lambda - c_r), sum 1."""
+    """group.cpp level_weights: trace shares s_r = max(0, lambda - c_r), sum 1 (then fr_group_create's sliver rule)."""
     c = sorted(cost)
     acc = 0.0
     lam = 0.0
@@ -38,7 +38,8 @@ def level_weights(cost):
         lam = (1.0 + acc) / k
         if k == len(c) or lam <= c[k]:
             break
-    return [max(0.0, lam - x) for x in cost]
+    w = [max(0.0, lam - x) for x in cost]
+    return [x if x >= 0.2 * max(w) else 0.0 for x in w]  # group.cpp: no slivers below a fifth of the largest share
 
 
 def main():
@@ -69,7 +70,12 @@ def main():
     assert src.shard_pack_active(slab.data_ptr(), n_all) == n_all
     src.destroy()
 
-    def pipelined(role_recon, n=K):
+    def pipelined(role_recon, n=K, every=1):
+        """ms per frame of K pipelined frames: role_recon None = whole one-GPU frames; else the trace half,
+        and (role_recon True) the other ranks' pixels scattered in and the reconstruction chains run on
+        every `every`-th frame (a rank taking JFA -> Sibson in turns with others, fr_group jfa_ranks)."""
+        state = {"f": 0}
+
         def one():
             if role_recon is None:
                 t.frame(timing=False)
@@ -77,37 +83,44 @@ def main():
             t.trace_frame(timing=False)
             if role_recon:
                 t.shard_unpack_active_enqueue(slab.data_ptr(), n_all, n_all)
-                t.reconstruct_frame(timing=False)
-        for _ in range(3):
+                if state["f"] % every == 0:
+                    t.reconstruct_frame(timing=False)
+            state["f"] += 1
+        for _ in range(3 * every):
             one()
         t.synchronize()
         t0 = time.perf_counter()
-        for _ in range(n):
+        for _ in range(n * every):
             one()
         t.synchronize()
-        return (time.perf_counter() - t0) / n * 1e3
+        return (time.perf_counter() - t0) / (n * every) * 1e3
 
     t.set_shard_plan(0, 1, T, np.zeros(1, np.uint8))
     t.set_recon_chains(3)
     one = pipelined(None)
     print(json.dumps({"G": 1, "scene": scene_name, "pipelined_frame_ms": round(one, 4), "fps": round(1e3 / one, 1),
                       "pixels_received_by_recon_ranks": n_all}), flush=True)
-    for G in (2, 4, 8):
-        cost = [RECON_COST[0] if r == 0 else RECON_COST[1] if r == 1 else 0.0 for r in range(G)]
+    for G, m in ((2, 1), (4, 1), (6, 1), (6, 2), (8, 1), (8, 2), (8, 3)):
+        # group.cpp's layout: view rank 0 and ranks 2..m take JFA -> Sibson in turns (cost / m each),
+        # view rank 1 pull-push -> A-Trous, the rest trace; tiles by water filling
+        jfa = [0] + list(range(2, m + 1))
+        cost = [(RECON_COST[0] / m if r in jfa else 0.0) + (RECON_COST[1] if r == 1 else 0.0) for r in range(G)]
         w = level_weights(cost)
         owner = fovrt.shard_plan(W, H, T, G, w)
         tiles = np.bincount(owner, minlength=G)
-        roles = {0: 1, 1: 2}
-        tracer = max(range(2, G), key=lambda r: tiles[r]) if G > 2 else None
-        if tracer is not None:
-            roles[tracer] = 0
+        roles = {r: 1 for r in jfa}
+        roles[1] = 2
+        tracers = [r for r in range(G) if r not in roles]
+        if tracers:
+            roles[max(tracers, key=lambda r: tiles[r])] = 0
         res = {}
         for r, chains in roles.items():
             t.set_shard_plan(r, G, T, owner)
+            t.set_front_local(chains == 0)  # group.cpp: a still camera's tracers run a tile-local front
             t.set_recon_chains(max(chains, 1))
             for form in (1, 2):
                 t.set_sample_sum(form)
-                ms = pipelined(chains != 0)
+                ms = pipelined(chains != 0, every=m if chains == 1 else 1)
                 res.setdefault(r, {"chains": chains, "tiles": int(tiles[r])})["pipelined_frame_ms_form%d" % form] = round(ms, 4)
             t.set_sample_sum(1)
             st = t.trace_frame(timing=True)
@@ -115,9 +128,11 @@ def main():
                            "trace_ms": round(st["geometry_ms"] + st["sampling_ms"] + st["optimize_ms"] + st["shading_ms"], 4),
                            "megakernel_ms": round(st["shade_paths_ms"], 4)})
             if chains:
+                t.shard_unpack_active_enqueue(slab.data_ptr(), n_all, n_all)
                 rt = t.reconstruct_frame(timing=True)
                 res[r]["recon_ms"] = round(rt["jfa_ms"] + rt["sibson_ms"] + rt["pullpush_ms"] + rt["atrous_ms"], 4)
-        out = {"G": G, "scene": scene_name, "weights": [round(x, 3) for x in w], "tiles": tiles.tolist(), "roles": res}
+        out = {"G": G, "jfa_ranks": m, "scene": scene_name, "weights": [round(x, 3) for x in w], "tiles": tiles.tolist(),
+               "roles": res}
         for form in (1, 2):
             frame = max(v["pipelined_frame_ms_form%d" % form] for v in res.values())
             out["model_frame_ms_form%d" % form] = round(frame, 4)

@@ -768,14 +768,16 @@ def test_gpu_bvh_follows_moved_triangles(fovrt_mod, oracle):
 # of the box (device-to-device copies), and a one-rank RCCL communicator. The group runs the same
 # frame as the reference's loop on one GPU, so every output equals the single-context frame.
 # ---------------------------------------------------------------------------------------------
-GROUP_CASES = [  # (ranks, views, tile, split, moving, W, H, mask)
-    (2, 1, 64, True, False, 200, 136, 4), (3, 1, 32, True, False, 200, 136, 4), (4, 1, 16, True, False, 200, 136, 0),
-    (3, 1, 32, False, False, 200, 136, 4), (4, 2, 32, True, False, 200, 136, 4), (2, 1, 32, True, True, 160, 112, 0),
-    (3, 1, 16, True, True, 160, 112, 4), (4, 1, 128, True, False, 3840, 2160, 4)]
+GROUP_CASES = [  # (ranks, views, tile, split, moving, W, H, mask, jfa_ranks)
+    (2, 1, 64, True, False, 200, 136, 4, 0), (3, 1, 32, True, False, 200, 136, 4, 0), (4, 1, 16, True, False, 200, 136, 0, 0),
+    (3, 1, 32, False, False, 200, 136, 4, 0), (4, 2, 32, True, False, 200, 136, 4, 0), (2, 1, 32, True, True, 160, 112, 0, 0),
+    (3, 1, 16, True, True, 160, 112, 4, 0), (4, 1, 128, True, False, 3840, 2160, 4, 0),
+    (4, 1, 32, True, False, 200, 136, 4, 2), (6, 2, 32, True, True, 160, 112, 4, 2), (4, 1, 16, True, False, 200, 136, 0, 3),
+    (8, 1, 128, True, False, 3840, 2160, 4, 0)]
 
 
-@pytest.mark.parametrize("R,V,tile,split,moving,W,H,mask", GROUP_CASES)
-def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving, W, H, mask):
+@pytest.mark.parametrize("R,V,tile,split,moving,W,H,mask,jfa", GROUP_CASES)
+def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving, W, H, mask, jfa):
     """fr_group_frame over R in-process ranks (V views of G = R / V): pipelined frames (no host sync but
     each rank's own front stages); with moving=True the camera pans every frame and every rank receives
     every other rank's traced pixels. Each view's reconstruction ranks hold the single-context frame's
@@ -795,7 +797,8 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
         cam.setPosition(np.asarray(cam.pos) + np.array([0.064 * (v - (V - 1) / 2), 0, 0], np.float32))
         cam.lookAt(cam.target)
         cams.append(cam)
-    g = fovrt_mod.Group(ranks, views=V, tile=tile, split_recon=split, moving_camera=moving, composite=True)
+    g = fovrt_mod.Group(ranks, views=V, tile=tile, split_recon=split, moving_camera=moving, composite=True,
+                        jfa_ranks=jfa)
     info = [g.rank_info(i) for i in range(R)]
     assert sum(i["tiles"] for i in info[:G]) == ((W + tile - 1) // tile) * ((H + tile - 1) // tile)
     for f in range(4):
@@ -812,17 +815,27 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
     out = torch.empty(V * W * H * 4, dtype=torch.float32, device="cuda")
     g.composite(out.data_ptr(), out.numel() * 4)
     comp = out.cpu().numpy().reshape(H, V * W, 4)
+    owners = g.tile_owners(W, H)
+    own_px = np.repeat(np.repeat(owners, tile, 0), tile, 1)[:H, :W]
     for v in range(V):
         full = fulls[v]
+        jfa_rank, at_rank = g.output_ranks(v)
+        m = jfa if jfa else (2 if split and G >= 6 else 1)  # the turns: view rank 0, 2, 3, ... one frame each
+        assert jfa_rank == v * G + (0 if 3 % m == 0 else 3 % m + 1) and at_rank == v * G + (1 if split and G > 1 else 0)
         for r in range(v * G, (v + 1) * G):
             ch = info[r]["chains"]
             if ch or moving:
                 for tid in (TN.SHADING, TN.HISTORY_CACHE):
                     assert equal_nan(ranks[r].read(tid), full.read(tid)), (v, r, tid)
-            if ch & 1:
+            else:  # a still camera's tracer runs a tile-local front: its own tiles equal the full frame
+                sel = own_px == r - v * G
+                for tid in (TN.SHADING, TN.HISTORY_CACHE, TN.MASK):
+                    assert equal_nan(ranks[r].read(tid)[sel], full.read(tid)[sel]), (v, r, tid)
+                assert ranks[r].stats()["gbuffer_primary"] < full.stats()["gbuffer_primary"]
+            if r == jfa_rank:
                 for tid in (TN.JFA_COLOR, TN.SIBSON):
                     assert equal_nan(ranks[r].read(tid), full.read(tid)), (v, r, tid)
-            if ch & 2:
+            if r == at_rank:
                 for tid in (TN.PULLPUSH, TN.ATROUS):
                     assert equal_nan(ranks[r].read(tid), full.read(tid)), (v, r, tid)
         assert equal_nan(comp[:, v * W:(v + 1) * W], full.read(TN.ATROUS)), v
