@@ -186,6 +186,12 @@ def main():
     ap.add_argument("--no-split", action="store_true",
                     help="both reconstruction chains on the view's rank 0 (default: JFA -> Sibson on view rank 0, "
                          "pull-push -> A-Trous on view rank 1)")
+    ap.add_argument("--jfa-ranks", type=int, default=0,
+                    help="view ranks taking JFA -> Sibson in turns, one frame each (fr_group_config.jfa_ranks; "
+                         "0 = auto: 2 at 6+ ranks per view, else 1)")
+    ap.add_argument("--no-front-local", action="store_true",
+                    help="every rank runs the full-screen front stages (default: a still camera's tracing ranks "
+                         "run them on their own tiles plus halo)")
     ap.add_argument("--recon-cost", type=float, nargs=2, default=None,
                     help="reconstruction work of view ranks 0 and 1 as fractions of a frame's trace work, for "
                          "the tile dealing (default: fr_group_config_default's)")
@@ -259,7 +265,8 @@ def main():
     group = None
     if R > 1:
         gkw = dict(views=views, tile=args.tile, split_recon=not args.no_split, moving_camera=args.pan != 0.0,
-                   composite=args.composite and views > 1, recon_cost=args.recon_cost)
+                   composite=args.composite and views > 1, recon_cost=args.recon_cost, jfa_ranks=args.jfa_ranks,
+                   front_local=not args.no_front_local)
         if world > 1:
             uid = broadcast_id(dist, rank, fovrt.rccl_unique_id)
             group = fovrt.Group.rccl(tracer, uid, world, rank, **gkw)
@@ -381,6 +388,8 @@ def main():
     img_bytes = sum(sb[k] for k in image_stages)
     img_ms = sum(avg[k] for k in image_stages)
     n_ranks = R
+    n_jfa = args.jfa_ranks or (2 if not args.no_split and G >= 6 else 1)  # group.cpp's auto rule
+    jfa_vranks = [0] + list(range(2, n_jfa + 1))
     if R == 1:
         parallelism = "one view on one GPU"
     elif G == 1:
@@ -389,8 +398,10 @@ def main():
         parallelism = (f"{views} view(s) x {G}-way {args.tile}px tile sharding (fr_group, tiles dealt by reconstruction "
                        f"load); traced pixels (20 B each) to the view's reconstruction ranks over RCCL "
                        f"ncclSend/ncclRecv; " + ("both chains on view rank 0" if args.no_split else
-                                                 "JFA -> Sibson on view rank 0, pull-push -> A-Trous on view rank 1") +
-                       (" (every rank receives every rank's pixels: moving camera)" if args.pan else ""))
+                                                 f"JFA -> Sibson on view rank(s) {jfa_vranks} in turns, pull-push -> "
+                                                 "A-Trous on view rank 1") +
+                       (" (every rank receives every rank's pixels: moving camera)" if args.pan else
+                        "" if args.no_front_local else "; tracing ranks run tile-local front stages"))
     if args.local_ranks > 1:
         parallelism += f"; REHEARSAL: {R} ranks as contexts of one process on one device (not a scaling measurement)"
     result = {
