@@ -130,6 +130,7 @@ def test_shading_within_tolerance(fovrt_mod, oracle, scene, spp, dmd, mask_mode,
         t.sampling_launch()
         t.optimize_launch()
         mask, weight, hist_in = t.read(TN.MASK), t.read(TN.WEIGHT), t.read(TN.HISTORY_CACHE)
+        gcls = t.read(TN.GCLASS)
         t.shading_launch()
         got_sh, got_hist = t.read(TN.SHADING), t.read(TN.HISTORY_CACHE)  # swapped: cache = just written
         ref = oracle.shading(osc, uni, W, H, frame, spp, mask, weight, hist_in)
@@ -138,6 +139,18 @@ def test_shading_within_tolerance(fovrt_mod, oracle, scene, spp, dmd, mask_mode,
         assert np.abs(np.nan_to_num(got_sh - ref["shading"], nan=1.0)).max() < 5e-2
         exact = np.mean(np.all(got_sh == ref["shading"], axis=-1))
         assert exact > 0.5, exact
+        # per primary-hit class of the traced pixels: each class's RMSE on its own, so a
+        # systematic error confined to one class (the refraction trees) cannot hide behind the others; misses
+        # differ only by the platform libm in the environment lookup
+        for c in range(4):
+            sel = (mask == 1) & (gcls == c)
+            if sel.sum() < 16:
+                continue
+            d = np.nan_to_num(got_sh[sel] - ref["shading"][sel], nan=1.0)
+            crm = np.sqrt(np.mean(d[:, :3] ** 2, 0))
+            assert (crm <= 1e-3).all(), (frame, c, crm)
+            if c == 3:
+                assert np.abs(d).max() <= 2e-3, (frame, np.abs(d).max())
         # inactive pixels carry history exactly; alpha is exactly 0 or 1 (App. A #14)
         inactive = mask == 0
         assert equal_nan(got_hist[inactive], ref["history"][inactive])
