@@ -349,13 +349,14 @@ def main():
 
     # Per-stage HIP-event breakdown of the same frames, serialised (each frame synchronised, so the
     # stage times do not overlap the next frame): the stage table and the roofline kernel time.
-    stage_ms = {}
+    stage_ms, stage_n = {}, {}
     n_timed = max(3, min(args.steps, 10))
     for _ in range(n_timed):
         tm = step(True)
         for k, v in tm.items():
             if k.endswith("_ms"):
                 stage_ms[k] = stage_ms.get(k, 0.0) + v
+                stage_n[k] = stage_n.get(k, 0) + (v > 0)
     for t in tracers:
         t.synchronize()
     # foveal density: every rank's active pixels of the last frame (a rank traces only its tiles)
@@ -363,7 +364,8 @@ def main():
     _, count_sum = reduce_over_ranks(dist, dev, 0.0, count_sum)
 
     K = args.steps
-    avg = {k[:-3]: v / n_timed for k, v in stage_ms.items()}
+    # (per stage over the frames that ran it: with jfa_ranks > 1 rank 0 runs JFA -> Sibson every m-th frame)
+    avg = {k[:-3]: v / max(1, stage_n[k]) for k, v in stage_ms.items()}
     rho = count_sum / views / (W * H)
     L = jfa_passes(W, H)
     sb = stage_bytes(W, H, rho, args.spp, L)
