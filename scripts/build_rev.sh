@@ -10,5 +10,5 @@ P=$WT/foveated-rendering-using-ray-tracing_amd
 mkdir -p "$ROOT/exp"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -w "$@" -shared \
   -o "$ROOT/exp/lib_$NAME.so" $P/csrc/k_trace.hip $P/csrc/k_image.hip $P/csrc/k_bvh.hip $P/csrc/scene.cpp \
-  $P/csrc/context.cpp -lz
+  $P/csrc/context.cpp $P/csrc/group.cpp -lz -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 git -C "$ROOT" worktree remove --force "$WT"
