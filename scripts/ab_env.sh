@@ -11,6 +11,6 @@ for i in $(seq 1 "$R"); do
   for spec in "$@"; do
     n=${spec%%:*}
     vars=${spec#*:}
-    env $vars timeout -k 10 200 python bench.py --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/rep_${n}_$i.log 2>&1 || exit 2
+    env $vars timeout -k 10 200 python bench.py --no-cpu-baseline --steps 40 --warmup 20 > gpurun_out/rep_${n}_$i.log 2>&1 || exit 2
   done
 done
