@@ -66,13 +66,16 @@ int view_of(const fr_group* g, int rank) { return rank / g->G; }
 int rank_of(const fr_group* g, int view, int vrank) { return view * g->G + vrank; }
 // The view ranks that take JumpFlooding -> Sibson in turns (one frame each): view rank 0, then 2, 3, ...
 // (view rank 1 runs pull-push -> A-Trous, whose push atlas carries state from frame to frame).
-bool runs_jfa(const fr_group* g, int vrank) { return vrank == 0 || (vrank >= 2 && vrank <= g->jfa_ranks); }
-int chains_of(const fr_group* g, int vrank) {
-  if (g->G == 1) return 3;
-  const bool split = g->cfg.split_recon != 0;
+int chains_for(int G, bool split, int jfa_ranks, int vrank) {
+  if (G == 1) return 3;
   if (vrank == 0) return split ? 1 : 3;
   if (vrank == 1 && split) return 2;
-  return runs_jfa(g, vrank) ? 1 : 0;
+  return vrank >= 2 && vrank <= jfa_ranks ? 1 : 0;
+}
+int chains_of(const fr_group* g, int vrank) { return chains_for(g->G, g->cfg.split_recon != 0, g->jfa_ranks, vrank); }
+// fr_group_config.jfa_ranks, with 0 = auto resolved
+int jfa_ranks_for(int G, const fr_group_config& cfg) {
+  return cfg.jfa_ranks ? cfg.jfa_ranks : (cfg.split_recon && G >= 6 ? 2 : 1);
 }
 // The view rank whose turn it is to run JumpFlooding -> Sibson on frame f.
 int jfa_turn(const fr_group* g, uint64_t f) {
@@ -101,6 +104,33 @@ void level_weights(const std::vector<double>& c, std::vector<float>& w) {
   }
   w.assign(n, 0.0f);
   for (int r = 0; r < n; r++) w[r] = (float)std::max(0.0, lambda - c[r]);
+}
+
+// The tile plan of a view of G ranks (fr_group_plan): explicit weights, or water filling on the
+// reconstruction loads followed by the sliver rule.
+int group_plan(int W, int H, int G, const fr_group_config& cfg, uint8_t* owner, size_t ntiles) {
+  std::vector<float> w(G, 0.0f);
+  bool explicit_w = false;
+  for (int r = 0; r < G; r++) explicit_w |= cfg.weights[r] != 0.0f;
+  if (explicit_w) {
+    for (int r = 0; r < G; r++) w[r] = cfg.weights[r];
+  } else {
+    const int m = jfa_ranks_for(G, cfg);
+    std::vector<double> cost(G, 0.0);
+    for (int r = 0; r < G; r++) {
+      const int ch = chains_for(G, cfg.split_recon != 0, m, r);
+      cost[r] = ((ch & 1) ? cfg.recon_cost[0] / m : 0.0) + ((ch & 2) ? cfg.recon_cost[1] : 0.0);
+    }
+    level_weights(cost, w);
+    // a rank left with a sliver of the tiles would still pay a whole launch's critical path (the
+    // longest refraction trees of a dense foveal tile take ~2 ms however few tiles there are), on top
+    // of its reconstruction chain: slivers below a fifth of the largest share go to the others
+    const float wmax = *std::max_element(w.begin(), w.end());
+    for (float& x : w) if (x < 0.2f * wmax) x = 0.0f;
+  }
+  if (int rc = fr_shard_plan(W, H, cfg.tile, G, w.data(), owner, ntiles))
+    return gfail(rc, std::string("group plan: ") + fr_last_error(nullptr));
+  return FR_OK;
 }
 
 int rccl_check(ncclResult_t r, const char* what) {
@@ -385,34 +415,15 @@ int fr_group_create(fr_ctx* const* ctxs, int n, void* rccl_comm, const fr_group_
     delete g;
     return gfail(FR_E_INVALID, "fr_group_create: jfa_ranks is 0 (auto) or 1 .. G - 1, and above 1 only with split_recon");
   }
-  g->jfa_ranks = cfg.jfa_ranks ? cfg.jfa_ranks : (cfg.split_recon && G >= 6 ? 2 : 1);
+  g->jfa_ranks = jfa_ranks_for(G, cfg);
   auto bail = [&](int rc) { fr_group_destroy(g); return rc; };
   // the tile plan (the same in every view)
   const int T = cfg.tile;
   const size_t ntiles = (size_t)((g->W + T - 1) / T) * ((g->H + T - 1) / T);
   g->tiles_per_vrank.assign(G, 0);
   if (G > 1) {
-    std::vector<float> w(G, 0.0f);
-    bool explicit_w = false;
-    for (int r = 0; r < G; r++) explicit_w |= cfg.weights[r] != 0.0f;
-    if (explicit_w) {
-      for (int r = 0; r < G; r++) w[r] = cfg.weights[r];
-    } else {
-      std::vector<double> cost(G, 0.0);
-      for (int r = 0; r < G; r++) {
-        const int ch = chains_of(g, r);
-        cost[r] = ((ch & 1) ? cfg.recon_cost[0] / g->jfa_ranks : 0.0) + ((ch & 2) ? cfg.recon_cost[1] : 0.0);
-      }
-      level_weights(cost, w);
-      // a rank left with a sliver of the tiles would still pay a whole launch's critical path (the
-      // longest refraction trees of a dense foveal tile take ~2 ms however few tiles there are), on top
-      // of its reconstruction chain: slivers below a fifth of the largest share go to the others
-      const float wmax = *std::max_element(w.begin(), w.end());
-      for (float& x : w) if (x < 0.2f * wmax) x = 0.0f;
-    }
     g->owner.resize(ntiles);
-    if (int rc = fr_shard_plan(g->W, g->H, T, G, w.data(), g->owner.data(), ntiles))
-      return bail(gfail(rc, std::string("fr_group_create: ") + fr_last_error(nullptr)));
+    if (int rc = group_plan(g->W, g->H, G, cfg, g->owner.data(), ntiles)) return bail(rc);
     for (uint8_t o : g->owner) g->tiles_per_vrank[o]++;
   }
   g->loc.resize(n);
@@ -548,6 +559,25 @@ int fr_group_rank_info(fr_group* g, int i, int* view, int* view_rank, int* chain
   if (chains) *chains = L.chains;
   if (tiles) *tiles = L.tiles;
   return FR_OK;
+}
+
+int fr_group_plan(int width, int height, int ranks_per_view, const fr_group_config* cfg_in, uint8_t* owner,
+                  size_t ntiles) {
+  if (!owner || width <= 0 || height <= 0) return gfail(FR_E_INVALID, "fr_group_plan: bad arguments");
+  fr_group_config cfg;
+  if (cfg_in) cfg = *cfg_in; else fr_group_config_default(&cfg);
+  const int G = ranks_per_view;
+  if (G < 1 || G > FR_GROUP_MAX_VIEW_RANKS) return gfail(FR_E_INVALID, "fr_group_plan: 1 <= ranks_per_view <= 16");
+  if (cfg.tile < 16 || cfg.tile % 16) return gfail(FR_E_INVALID, "fr_group_plan: tile must be a multiple of 16");
+  if (cfg.jfa_ranks < 0 || cfg.jfa_ranks > 1 + std::max(0, G - 2) || (cfg.jfa_ranks > 1 && !cfg.split_recon))
+    return gfail(FR_E_INVALID, "fr_group_plan: jfa_ranks is 0 (auto) or 1 .. G - 1, and above 1 only with split_recon");
+  const size_t nt = (size_t)((width + cfg.tile - 1) / cfg.tile) * ((height + cfg.tile - 1) / cfg.tile);
+  if (ntiles != nt) return gfail(FR_E_INVALID, "fr_group_plan: ntiles != ceil(W/tile) * ceil(H/tile)");
+  if (G == 1) {
+    memset(owner, 0, nt);
+    return FR_OK;
+  }
+  return group_plan(width, height, G, cfg, owner, nt);
 }
 
 int fr_group_output_ranks(fr_group* g, int view, int* jfa_rank, int* atrous_rank) {

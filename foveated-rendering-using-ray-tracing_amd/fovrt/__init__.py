@@ -182,6 +182,7 @@ _SIGS = {
                            C.POINTER(C.c_int)],
     "fr_group_tile_owners": [C.c_void_p, C.c_void_p, C.c_size_t],
     "fr_group_output_ranks": [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "fr_group_plan": [C.c_int, C.c_int, C.c_int, C.POINTER(fr_group_config), C.c_void_p, C.c_size_t],
     "fr_group_synchronize": [C.c_void_p],
     "fr_group_destroy": [C.c_void_p],
     "fr_group_last_error": [],
@@ -715,6 +716,26 @@ def shard_plan(width, height, tile, count, weights=None) -> np.ndarray:
                            owner.ctypes.data_as(C.POINTER(C.c_uint8)), nt)
     if rc:
         raise FovrtError(rc, lib.fr_last_error(None).decode())
+    return owner
+
+
+def group_plan(width, height, ranks_per_view, tile=128, split_recon=True, recon_cost=None, weights=None,
+               jfa_ranks=0) -> np.ndarray:
+    """fr_group_plan (host only): the tile plan fr_group_create deals for one view (view rank per tile)."""
+    lib = load_library()
+    cfg = fr_group_config()
+    lib.fr_group_config_default(C.byref(cfg))
+    cfg.tile, cfg.split_recon, cfg.jfa_ranks = int(tile), int(bool(split_recon)), int(jfa_ranks)
+    if recon_cost is not None:
+        cfg.recon_cost[0], cfg.recon_cost[1] = float(recon_cost[0]), float(recon_cost[1])
+    if weights is not None:
+        for i, w in enumerate(weights):
+            cfg.weights[i] = float(w)
+    nt = ((width + tile - 1) // tile) * ((height + tile - 1) // tile)
+    owner = np.zeros(nt, np.uint8)
+    rc = lib.fr_group_plan(int(width), int(height), int(ranks_per_view), C.byref(cfg), owner.ctypes.data, nt)
+    if rc:
+        raise FovrtError(rc, lib.fr_group_last_error().decode())
     return owner
 
 

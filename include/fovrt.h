@@ -348,6 +348,9 @@ int fr_group_composite(fr_group* g, void* out, size_t bytes);
 /* Roles of local rank i: *view, *view_rank, *chains (bit 0 JFA -> Sibson, bit 1 pull-push -> A-Trous
  * run here) and *tiles, the number of screen tiles it traces. */
 int fr_group_rank_info(fr_group* g, int i, int* view, int* view_rank, int* chains, int* tiles);
+/* Host only (no device): the tile plan fr_group_create would deal for one view of ranks_per_view ranks
+ * (cfg NULL = fr_group_config_default): owner[t] = the view rank tracing tile t. */
+int fr_group_plan(int width, int height, int ranks_per_view, const fr_group_config* cfg, uint8_t* owner, size_t ntiles);
 /* Where the last frame's outputs of a view are: the global rank holding its JFA / Sibson images (the
  * rank whose turn it was, see jfa_ranks) and the one holding its pull-push / A-Trous images. */
 int fr_group_output_ranks(fr_group* g, int view, int* jfa_rank, int* atrous_rank);

@@ -29,10 +29,7 @@ def main():
     # rank) in the sample-sum form FR_TRACE_FORM (the group default 2)
     G = int(os.environ.get("FR_TRACE_G", "1"))
     if G > 1:
-        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-        from shard_model import level_weights, RECON_COST
-        cost = [RECON_COST[0] if r == 0 else RECON_COST[1] if r == 1 else 0.0 for r in range(G)]
-        owner = fovrt.shard_plan(W, H, 128, G, level_weights(cost))
+        owner = fovrt.group_plan(W, H, G)
         t.set_shard_plan(int(os.environ.get("FR_TRACE_RANK", "2")), G, 128, owner)
         t.set_sample_sum(int(os.environ.get("FR_TRACE_FORM", "2")))
         t.set_recon_chains(1)

@@ -131,3 +131,29 @@ def test_shard_plan_deals_tiles_by_weight():
         fovrt.shard_plan(W, H, 8, 4)  # tiles are multiples of 16
     with pytest.raises(fovrt.FovrtError):
         fovrt.shard_plan(W, H, T, 2, [0.0, 0.0])
+
+
+def test_group_plan_layouts():
+    """fr_group_plan (host only) is the plan fr_group_create deals: water filling on the reconstruction
+    loads (view rank 0 JFA -> Sibson, 1 pull-push -> A-Trous), JFA -> Sibson in turns on ranks 0 and 2 from
+    six ranks per view, and no sliver shares (below a fifth of the largest go to the others)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)),
+                                    "foveated-rendering-using-ray-tracing_amd"))
+    import fovrt
+    W, H = 3840, 2160
+    counts = {G: np.bincount(fovrt.group_plan(W, H, G), minlength=G).tolist() for G in (1, 2, 4, 6, 8)}
+    assert counts[1] == [510]
+    assert counts[2] == [171, 339]
+    assert counts[4] == [0, 112, 199, 199]
+    assert counts[6] == [0, 59, 0, 151, 150, 150]          # jfa_ranks auto = 2: ranks 0 and 2 trace nothing
+    assert counts[8] == [0, 0, 0, 102, 102, 102, 102, 102]  # rank 1's sliver (0.025) goes to the tracers
+    assert np.bincount(fovrt.group_plan(W, H, 8, jfa_ranks=1), minlength=8).tolist() == [0, 0] + [85] * 6
+    # no split: rank 0 runs both chains
+    assert np.bincount(fovrt.group_plan(W, H, 3, split_recon=False), minlength=3)[0] == 0
+    # explicit weights bypass the rule
+    assert np.bincount(fovrt.group_plan(W, H, 2, weights=[1, 1]), minlength=2).tolist() == [255, 255]
+    with pytest.raises(fovrt.FovrtError):
+        fovrt.group_plan(W, H, 4, jfa_ranks=4)  # at most G - 1
+    with pytest.raises(fovrt.FovrtError):
+        fovrt.group_plan(W, H, 4, jfa_ranks=2, split_recon=False)
