@@ -201,7 +201,10 @@ def load_library(path: str | None = None):
         raise FovrtError(FR_E_STATE, f"{path} not built: run __graft_entry__.build() or make -C "
                                      f"foveated-rendering-using-ray-tracing_amd")
     lib = C.CDLL(path)
+    older = path != LIB_PATH and os.environ.get("FOVRT_LIB_OLDER") == "1"  # A/B against an older build
     for name, args in _SIGS.items():
+        if older and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = C.c_char_p if name in ("fr_version", "fr_last_error", "fr_group_last_error") else C.c_int
