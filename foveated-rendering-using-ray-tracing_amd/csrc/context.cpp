@@ -698,9 +698,7 @@ static int enqueue_shading(fr_ctx* c) {
   if (kt) hipEventRecord(kt[1], c->stream);
   launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache],
                      c->shade_ctr, c->samples, c->sample_help, c->stats, c->aux, c->aux_seed, c->chunk_refr,
-                     c->xcd_bands, c->handoff, c->item_store,
-                     /* leave_one: a context running the whole frame leaves its other streams room */
-                     c->recon_chains == 3 && c->U.shard_count <= 1, c->stream);
+                     c->xcd_bands, c->handoff, c->item_store, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[10], c->stream);
   if (kt) hipEventRecord(kt[2], c->stream);
   hipStreamWaitEvent(c->stream, c->ev[12], 0);

@@ -16,7 +16,7 @@ namespace fr {
 void launch_gbuffer(const DevScene&, const FrameUniforms&, f4*, f4*, f4*, f4*, f4*, uint8_t*, DevStats*, hipStream_t);
 void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*,
                         const f4*, uint32_t*, f4*, unsigned long long*, DevStats*, f4*, uint32_t*, uint32_t, uint32_t,
-                        uint32_t, f4*, bool, hipStream_t);
+                        uint32_t, f4*, hipStream_t);
 size_t shade_item_store_f4();
 void launch_sample_setup(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*, f4*,
                          uint32_t*, hipStream_t);
