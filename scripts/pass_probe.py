@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """One reconstruction pass alone at 4K on the bench frame's shading, K times (A/B timing of library
-variants, FOVRT_LIB=...): python scripts/pass_probe.py <jfa|sibson|pullpush|atrous> [K]"""
+variants, FOVRT_LIB=... or an env knob; FR_PASS_DUMP=<file.npy> saves the pass's output): python scripts/pass_probe.py <jfa|sibson|pullpush|atrous> [K]"""
 import os
 import sys
 import numpy as np
@@ -21,4 +21,8 @@ p = {"jfa": fovrt.JumpFlooding, "sibson": fovrt.SibsonInterpolation, "pullpush":
      "atrous": fovrt.ATrous}[name](t)
 ms = [p.render() / 1e6 for _ in range(K)]
 print(f"{name} median {np.median(ms):.4f} ms min {np.min(ms):.4f} (K={K})")
+if os.environ.get("FR_PASS_DUMP"):  # the pass's output, for bit-exact comparisons between variants
+    out = {"jfa": fovrt.TextureName.JFA_COLOR, "sibson": fovrt.TextureName.SIBSON,
+           "pullpush": fovrt.TextureName.PULLPUSH, "atrous": fovrt.TextureName.ATROUS}[name]
+    np.save(os.environ["FR_PASS_DUMP"], t.read(out))
 t.destroy()

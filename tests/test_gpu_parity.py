@@ -315,10 +315,10 @@ def test_pullpush_bit_exact_across_frames(fovrt_mod, oracle, W, H):
         assert equal_nan(got, npst.render(img)), k
 
 
+@pytest.mark.parametrize("W,H", [(80, 60), (203, 77)])  # the second: ragged 16x16 blocks, interior and edge
 @pytest.mark.parametrize("count", [1, 2, 3])
-def test_atrous_within_tolerance(fovrt_mod, oracle, count):
-    W, H = 80, 60
-    rng = np.random.default_rng(count)
+def test_atrous_within_tolerance(fovrt_mod, oracle, count, W, H):
+    rng = np.random.default_rng(count + W)
     t = _box_tracer(fovrt_mod, W, H)
     pos, nrm, col = (rng.random((H, W, 4), dtype=np.float32) for _ in range(3))
     t.write(TN.POSITION, pos)
