@@ -78,6 +78,28 @@ SAMPLING_CASES = ([(scene, m, 128, 96, None) for scene in (1, 2) for m in (0, 1,
                      (1, 0, 128, 96, (1e6, -1e6))])
 
 
+@pytest.mark.parametrize("mask_mode", [0, 1, 2, 3, 4])
+def test_sampling_without_extra_bit_exact(fovrt_mod, oracle, mask_mode):
+    """write_extra = 0: k_sampling skips the saliency features unless the saliency mask reads them; the
+    mask and WEIGHT stay the oracle's, and EXTRA is left untouched."""
+    W, H = 100, 70
+    t = make_tracer(fovrt_mod, W, H, scene=1, mask=mask_mode, write_extra=0)
+    uni = fovrt_mod.Camera.preset(1, W, H).uniforms(W, H)
+    t.set_camera_uniforms(uni)
+    osc = oracle.OracleScene(t.scene_arrays())
+    before = t.read(TN.EXTRA)
+    for frame in range(2):
+        t.geometry_launch()
+        inp = [t.read(v) for v in (TN.POSITION, TN.DEPTH, TN.DEPTH_CACHE, TN.WEIGHT, TN.NORMAL, TN.DIFFUSE)]
+        t.sampling_launch()
+        ref = oracle.sampling(osc, uni, W, H, mask_mode, *inp)
+        assert np.array_equal(t.read(TN.MASK), ref["mask"]), (frame, mismatch_report(t.read(TN.MASK), ref["mask"]))
+        assert equal_nan(t.read(TN.WEIGHT), ref["weight"]), frame
+        t.optimize_launch()
+        t.shading_launch()
+    assert equal_nan(t.read(TN.EXTRA), before)
+
+
 @pytest.mark.parametrize("scene,mask_mode,W,H,gaze_window", SAMPLING_CASES)
 def test_sampling_and_compaction_bit_exact(fovrt_mod, oracle, scene, mask_mode, W, H, gaze_window):
     t = make_tracer(fovrt_mod, W, H, scene=scene, mask=mask_mode)
