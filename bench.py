@@ -159,9 +159,13 @@ def load_traffic(kernels, config):
         if any(cfg.get(k) != config.get(k) for k in ("scene", "width", "height", "spp", "diffuse_max_depth",
                                                      "mask_mode")):
             continue
-        ks = doc.get("kernels", {})
-        if all(k in ks for k in kernels):
-            return sum(ks[k]["hbm_bytes"] for k in kernels), os.path.relpath(path, ROOT)
+        # by base name: "void k_carry_history<false>" is k_carry_history (every template instance counts)
+        base = {}
+        for name, v in doc.get("kernels", {}).items():
+            b = name.split("<")[0].split("(")[0].split()[-1] if name.strip() else ""
+            base[b] = base.get(b, 0.0) + v["hbm_bytes"]
+        if all(k in base for k in kernels):
+            return sum(base[k] for k in kernels), os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -385,7 +389,7 @@ def main():
                       f"({live['frames']} pipelined frames)")
     achieved = sb[dominant] / (launch_ms * 1e-3) / 1e9
     stage_kernels = {"shading": ["k_shade_paths", "k_shade_resolve", "k_carry_history"],
-                     "geometry": ["k_gbuffer"], "sibson": ["k_sibson"]}
+                     "geometry": ["k_gbuffer"], "sibson": ["k_sibson_runs"]}
     image_stages = ["sampling", "optimize", "jfa", "sibson", "pullpush", "atrous"]
     img_bytes = sum(sb[k] for k in image_stages)
     img_ms = sum(avg[k] for k in image_stages)
