@@ -41,7 +41,7 @@ void launch_shard_pack_active(const uint32_t*, const uint32_t*, uint32_t, const 
 void launch_shard_unpack_active(const f4*, const uint32_t*, uint32_t, uint32_t, f4*, f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, f4*, f4*, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
-void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, int, int, bool, hipStream_t);
+void launch_sibson_runs(const f4*, const f4*, f4*, f4*, uint32_t*, f4*, int, int, bool, hipStream_t);
 int sibson_prefix_blocks(int W);
 struct BvhWork;
 bool gpu_build_bvh(BvhWork**, const f3*, int, BvhNode*, TriGeo*, int32_t*, int*, int*, int*, hipStream_t, std::string&);
@@ -186,6 +186,7 @@ struct fr_ctx {
   float* ftab = nullptr;  // texel-centre coordinates ((x + 0.5) / W, x < W; then (y + 0.5) / H)
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
   f4 *sib_prefix = nullptr, *sib_blocks = nullptr;  // Sibson run form: per-row block prefix sums + block totals
+  uint32_t* sib_wide = nullptr;  // Sibson run form: wide-disc pixel list (count, then W*H indices)
   bool sib_prefix_fresh = false;  // the last JFA wrote them with JFA_COLOR (cleared when JFA_COLOR is written)
   int pp_S = 0;
   DevStats* stats = nullptr;

@@ -9,8 +9,8 @@ never leaks into the next stage's comparison.
 import numpy as np
 import pytest
 
-from helpers import (GOLDEN, TEXTURE_MODE, ASSET_DIR, PullPushNp, atrous_np, equal_nan, logpolar_mask_np,
-                     rmse_per_channel, sparse_image)
+from helpers import (GOLDEN, TEXTURE_MODE, ASSET_DIR, PullPushNp, _gl_linear_repeat, atrous_np, equal_nan,
+                     logpolar_mask_np, rmse_per_channel, sparse_image)
 
 pytestmark = pytest.mark.gpu
 
@@ -319,6 +319,95 @@ def test_sibson_run_form_full_size(fovrt_mod, W, H):
     assert np.isfinite(b).all() and np.array_equal(a[..., 3], b[..., 3])
     assert np.abs(a - b).max() <= SIB_RUN_MAX, np.abs(a - b).max()
     assert (rmse_per_channel(a, b) <= SIB_RUN_RMSE).all(), rmse_per_channel(a, b)
+
+
+def _jfa_then_run_form(fovrt_mod, img, W, H):
+    """JFA on the image (per-tap context), then the default run-form Sibson on its output."""
+    ex = _box_tracer(fovrt_mod, W, H)
+    ex.write(TN.SHADING, img)
+    fovrt_mod.JumpFlooding(ex).render(TN.SHADING)
+    coord, color = ex.read(TN.JFA_COORD), ex.read(TN.JFA_COLOR)
+    ru = make_tracer(fovrt_mod, W, H, scene=0, mask=3, sibson_mode=0)
+    ru.write(TN.JFA_COORD, coord)
+    ru.write(TN.JFA_COLOR, color)
+    si = fovrt_mod.SibsonInterpolation(ru)
+    ns = min(si.render() for _ in range(2))  # (the first call also loads the kernels)
+    return coord, color, ru.read(TN.SIBSON), ns
+
+
+@pytest.mark.parametrize("W,H,kind", [(160, 120, "few"), (97, 61, "corner"), (256, 144, "few"), (130, 70, "edge")])
+def test_sibson_run_form_wide_discs(fovrt_mod, oracle, W, H, kind):
+    """Discs spanning most of the image (a handful of seeds: the holes an off-centre log-polar gaze
+    leaves, scripts/gaze_probe.py). Their boxes cross the binade edges of the tap positions and the
+    image border, so the pixels take k_sibson_wide's segment tables; against the oracle's per-tap
+    Sibson (sibsonFS.glsl:16-49)."""
+    rng = np.random.default_rng(W * 7 + H)
+    m = np.zeros((H, W), np.uint8)
+    if kind == "few":
+        m[rng.integers(0, H, 5), rng.integers(0, W, 5)] = 1
+    elif kind == "corner":
+        m[0, 0] = m[2, 1] = 1
+    else:  # seeds along the right border only: discs reach across the left border
+        m[::17, W - 1] = 1
+    img = sparse_image(W, H, m, seed=W + H)
+    coord, color, sf, _ = _jfa_then_run_form(fovrt_mod, img, W, H)
+    rs = oracle.sibson(coord, color)
+    assert np.isfinite(sf).all() and np.array_equal(sf[..., 3], rs[..., 3])
+    assert np.abs(sf - rs).max() <= SIB_RUN_MAX, np.abs(sf - rs).max()
+    assert (rmse_per_channel(sf, rs) <= SIB_RUN_RMSE).all(), rmse_per_channel(sf, rs)
+
+
+def _sibson_pixel_np(coord, color, x, y):
+    """One pixel of sibsonFS.glsl:16-49 in numpy: the shader's f32 position sequences (h, w += 1/size)
+    walked in order, the taps outside [0, 1) or the disc dropped, GL_LINEAR + REPEAT at each tap
+    (8-bit weights), summed in f64 (any order: the run form's own order differs)."""
+    f = np.float32
+    H, W = coord.shape[:2]
+    fx, fy = f((f(x) + f(0.5)) / f(W)), f((f(y) + f(0.5)) / f(H))
+    cs, ct = coord[y, x, 0], coord[y, x, 1]
+    dx, dy = f(cs - fx), f(ct - fy)
+    d = f(np.sqrt(f(f(dx * dx) + f(dy * dy))))
+
+    def seq(lo, hi, inc):
+        out, v = [], lo
+        while v < hi:
+            out.append(v)
+            v = f(v + inc)
+        return np.array(out, f)
+
+    ws = seq(f(fx - d), f(fx + d), f(f(1) / f(W)))
+    hs = seq(f(fy - d), f(fy + d), f(f(1) / f(H)))
+    ww, hh = np.meshgrid(ws, hs)
+    r = np.sqrt(f(f(f(fx - ww) ** 2) + f(f(fy - hh) ** 2)), dtype=f)
+    on = (ww >= 0) & (ww < 1) & (hh >= 0) & (hh < 1) & ~(r > d)
+    if not on.any():
+        return None
+    c = _gl_linear_repeat(color, ww[on], hh[on]).astype(np.float64)
+    return c[:, :3].sum(0) / on.sum()
+
+
+def test_sibson_run_form_offcentre_gaze_4k(fovrt_mod):
+    """The 4K log-polar mask of bench.py --gaze-path's cursor at 180 degrees (gaze (1380, 1080)) leaves
+    holes whose discs reach ~1,100 rows: the widest pixels (k_sibson_wide) and a sample of the rest
+    against the shader's per-pixel loops; the whole pass must stay far from the 150-430 ms that the
+    per-lane tap walk took there."""
+    W, H = 3840, 2160
+    mask = logpolar_mask_np(W, H, 1380, 1080, signed=True)
+    img = sparse_image(W, H, mask, seed=11)
+    coord, color, sf, ns = _jfa_then_run_form(fovrt_mod, img, W, H)
+    assert np.isfinite(sf).all()
+    yy, xx = np.mgrid[0:H, 0:W]
+    d = np.hypot(coord[..., 0] - (xx + 0.5) / W, coord[..., 1] - (yy + 0.5) / H)
+    rng = np.random.default_rng(5)
+    wide = np.argsort(d.ravel())[-400:]
+    pick = np.concatenate([rng.choice(wide, 12, replace=False), rng.choice(W * H, 12, replace=False),
+                           [int(np.argmax(d))]])
+    for p in pick:
+        y, x = divmod(int(p), W)
+        ref = _sibson_pixel_np(coord, color, x, y)
+        assert ref is not None and sf[y, x, 3] == 1.0, (x, y)
+        assert np.abs(sf[y, x, :3] - ref).max() <= SIB_RUN_MAX, (x, y, d[y, x] * H, sf[y, x, :3], ref)
+    assert ns / 1e6 < 60.0, ns / 1e6
 
 
 @pytest.mark.parametrize("W,H", [(64, 64), (96, 64), (256, 256), (130, 70)])
