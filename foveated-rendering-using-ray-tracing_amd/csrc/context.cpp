@@ -473,7 +473,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       hipMalloc((void**)&c->item_store, shade_item_store_f4() * sizeof(f4)) != hipSuccess ||
       (cfg.sibson_mode == 0 && (dalloc(&c->sib_prefix, (size_t)(c->W + 1) * c->H) != hipSuccess ||
                                 dalloc(&c->sib_blocks, (size_t)sibson_prefix_blocks(c->W) * c->H) != hipSuccess ||
-                                hipMalloc((void**)&c->sib_wide, ((size_t)c->W * c->H + 1) * sizeof(uint32_t)) != hipSuccess))) {
+                                hipMalloc((void**)&c->sib_wide, ((size_t)c->W * c->H + 2) * sizeof(uint32_t)) != hipSuccess))) {
     c->err = "device allocation (work buffers) failed";
     return bail(FR_E_NOMEM);
   }

@@ -186,7 +186,7 @@ struct fr_ctx {
   float* ftab = nullptr;  // texel-centre coordinates ((x + 0.5) / W, x < W; then (y + 0.5) / H)
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
   f4 *sib_prefix = nullptr, *sib_blocks = nullptr;  // Sibson run form: per-row block prefix sums + block totals
-  uint32_t* sib_wide = nullptr;  // Sibson run form: wide-disc pixel list (count, then W*H indices)
+  uint32_t* sib_wide = nullptr;  // Sibson run form: wide-disc pixel lists (two counts, then W*H indices)
   bool sib_prefix_fresh = false;  // the last JFA wrote them with JFA_COLOR (cleared when JFA_COLOR is written)
   int pp_S = 0;
   DevStats* stats = nullptr;
