@@ -53,10 +53,11 @@ def jfa_passes(W, H):
     return int(np.log2(m)) + 1
 
 
-def cpu_baseline(args, cfg_scene_arrays, cam_uni_fn):
+def cpu_baseline(args, cfg_scene_arrays, cam_uni_fn, gpu_segments_per_frame=None):
     """The CPU oracle (oracle/, a literal restatement of the reference path, OpenMP over rows) timed on
-    this host on a bounded sample: the full bench workload (same scene/resolution/spp/GI/mask), two
-    frames, the second one timed (frame 0 only establishes the temporal history)."""
+    this host on a bounded sample of the same workload (scene, resolution, spp, GI, mask), SURVEY §8(d)'s
+    method shortened to fit the bench: frame 0 is the warm-up (it also establishes the temporal history),
+    frames 1..3 are timed and the median is reported."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
     W, H = args.width // args.cpu_scale, args.height // args.cpu_scale
@@ -66,8 +67,8 @@ def cpu_baseline(args, cfg_scene_arrays, cam_uni_fn):
     hist = np.zeros((H, W, 4), np.float32)
     depth_cache = np.zeros((H, W, 4), np.float32)
     pp = po.PullPushState(W, H)
-    t_total, segs, t_all = 0.0, 0, time.perf_counter()
-    for frame in range(2):
+    times, segs, t_all = [], [], time.perf_counter()
+    for frame in range(1 + args.cpu_frames):
         sc.segments(reset=True)
         t0 = time.perf_counter()
         g = po.gbuffer(sc, uni, W, H, frame)
@@ -81,16 +82,35 @@ def cpu_baseline(args, cfg_scene_arrays, cam_uni_fn):
         po.atrous(1, g["position"], g["normal"], out)
         dt = time.perf_counter() - t0
         hist, depth_cache = sh["history"], g["depth"]
-        if frame == 1:
-            t_total, segs = dt, sc.segments(reset=True)
+        if frame >= 1:
+            times.append(dt)
+            segs.append(sc.segments(reset=True))
+    t_med = float(np.median(times))
+    seg_med = float(np.median(segs))
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     scale = "" if args.cpu_scale == 1 else f" at 1/{args.cpu_scale} x 1/{args.cpu_scale} resolution"
-    return {"value": round(segs / t_total / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "sample": f"oracle (OpenMP) full frame {W}x{H}{scale}, same scene/spp/GI/mask as the GPU workload; "
-                      f"frame 0 untimed (history), frame 1 timed: {segs} ray segments counted as the reference "
-                      f"traces them (incl. rays whose results it never reads) in {t_total:.2f} s "
-                      f"({time.perf_counter() - t_all:.1f} s of CPU work in total)",
-            "frame_s": round(t_total, 3), "fps": round(1.0 / t_total, 4)}
+    res = {"value": round(seg_med / t_med / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
+           "sample": f"oracle (OpenMP) full frames {W}x{H}{scale}, same scene/spp/GI/mask as the GPU workload; "
+                     f"frame 0 the warm-up (it builds the history), median of frames 1-{args.cpu_frames} timed "
+                     f"({', '.join(f'{t:.2f}' for t in times)} s); {time.perf_counter() - t_all:.1f} s of CPU work "
+                     f"in total",
+           "frame_s": round(t_med, 3), "frames_s": [round(t, 3) for t in times], "fps": round(1.0 / t_med, 4),
+           "segments_per_frame": int(seg_med),
+           "segments_definition": "every segment the reference traces, including the G-buffer shadow rays whose "
+                                  "result g_diffuse.cu:110-143 never reads and the grandchildren diffuse.cu:142 / "
+                                  "reflection.cu:144 discard (the GPU engine does not trace those: its "
+                                  "segments_per_frame counts only segments traced), so Mrays/s ratios mix two "
+                                  "definitions; compare fps"}
+    if gpu_segments_per_frame:
+        res["gpu_segments_per_frame"] = int(gpu_segments_per_frame)
+    return res
+
+
+def pct(a):
+    """p50 / p99 / max / mean of a sample of milliseconds."""
+    a = np.asarray(a, np.float64)
+    return {"p50": round(float(np.median(a)), 4), "p99": round(float(np.percentile(a, 99)), 4),
+            "max": round(float(a.max()), 4), "mean": round(float(a.mean()), 4), "n": int(a.size)}
 
 
 def view_offset(rank, world):
@@ -183,6 +203,9 @@ def main():
     ap.add_argument("--refraction-max-depth", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-scale", type=int, default=1, help="CPU baseline at 1/scale resolution per axis")
+    ap.add_argument("--cpu-frames", type=int, default=3, help="CPU baseline: timed frames after the warm-up")
+    ap.add_argument("--serial-frames", type=int, default=50,
+                    help="frames of the serial frame-time measurement (after 5 warm-ups; SURVEY §8(d))")
     ap.add_argument("--views", type=int, default=1,
                     help="views rendered by the job (default 1: one 4K view tile-sharded over all ranks, strong "
                          "scaling; --views N with N ranks: one view per rank, weak scaling)")
@@ -211,9 +234,11 @@ def main():
                     help="per-frame step of the camera's look-at target in scene units (0: static camera). A "
                          "moving camera makes the history reprojection read across tiles; every rank of a "
                          "tile-sharded view then receives every other rank's traced pixels")
-    ap.add_argument("--gaze-path", action="store_true",
-                    help="the gaze follows a scripted cursor path every frame (cursorPosCallback, FR/gui.cpp:48-66): "
-                         "the log-polar mask is recomputed every frame (an eye-tracked frame)")
+    ap.add_argument("--gaze-path", nargs="?", const="circle", default=None, choices=["circle", "saccade"],
+                    help="the gaze follows a scripted cursor path every frame (cursorPosCallback, FR/gui.cpp:48-66), "
+                         "so the mask is recomputed every frame (an eye-tracked frame): 'circle' (the bare flag) "
+                         "circles the screen centre at a quarter of the height, one degree per frame; 'saccade' "
+                         "jumps 90 degrees along the same circle every 30 frames")
     args = ap.parse_args()
     args.mask = fovrt.MASKS[args.mask]
     scene = fovrt.SCENES[args.scene]
@@ -295,7 +320,8 @@ def main():
     def move_gaze():
         """A scripted cursor (window coordinates, y down) circling the screen centre at a quarter of the
         height, one degree per frame, fed through cursorPosCallback's mapping (fr_set_gaze, windowed)."""
-        a = np.deg2rad(frame_no[0])
+        deg = frame_no[0] if args.gaze_path == "circle" else 90 * (frame_no[0] // 30)
+        a = np.deg2rad(deg)
         x = W / 2 + 0.25 * H * np.cos(a)
         y = (H / 2 + 0.25 * H * np.sin(a)) / 1.25  # the callback scales y by 1.25 in a window
         for t in tracers:
@@ -326,6 +352,8 @@ def main():
     # reconstruction runs while frame N+1 traces). Entry 3 (the roofline stage) is timed live inside it:
     # HIP events on the context stream around the stage and its megakernel, no synchronisation added.
     tracer.kernel_timing(True)
+    if group is None:
+        tracer.frame_clock(True)  # per-frame latency (gaze -> image) and display interval, HIP events
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -340,6 +368,12 @@ def main():
     elapsed = time.perf_counter() - t0
     live = tracer.kernel_times()
     tracer.kernel_timing(False)
+    clock = None
+    if group is None:
+        lat, itv = tracer.frame_clock_read()
+        tracer.frame_clock(False)
+        if len(lat) and len(itv):
+            clock = {"latency_ms": pct(lat), "interval_ms": pct(itv)}
 
     segs = redundant = 0
     for (view, vrank, g), t in zip(layouts, tracers):
@@ -353,14 +387,22 @@ def main():
 
     # Per-stage HIP-event breakdown of the same frames, serialised (each frame synchronised, so the
     # stage times do not overlap the next frame): the stage table and the roofline kernel time.
+    # The same frames are SURVEY §8(d)'s reconstructed-frame time: HIP events around one whole
+    # synchronised frame (update -> entries 0-3 -> JFA -> Sibson -> pull-push -> A-Trous, nothing of the
+    # next frame overlapping), the median of --serial-frames after 5 warm-ups.
     stage_ms, stage_n = {}, {}
-    n_timed = max(3, min(args.steps, 10))
+    for _ in range(5):
+        step(True)
+    n_timed = max(3, args.serial_frames)
+    totals = []
     for _ in range(n_timed):
         tm = step(True)
+        totals.append(tm["total_ms"])
         for k, v in tm.items():
             if k.endswith("_ms"):
                 stage_ms[k] = stage_ms.get(k, 0.0) + v
                 stage_n[k] = stage_n.get(k, 0) + (v > 0)
+    serial = pct(np.asarray(totals, np.float64))
     for t in tracers:
         t.synchronize()
     # foveal density: every rank's active pixels of the last frame (a rank traces only its tiles)
@@ -429,11 +471,26 @@ def main():
                    "scene": args.scene, "width": W, "height": H, "spp": args.spp, "diffuse_max_depth": args.dmd,
                    "mask_mode": args.mask, "foveal_density": round(rho, 5), "views": views, "ranks": n_ranks,
                    "composite": bool(args.composite and views > 1), "camera_step": args.pan,
-                   "gaze": "scripted cursor path, mask recomputed every frame" if args.gaze_path else "screen centre",
+                   "gaze": {None: "screen centre",
+                            "circle": "scripted cursor circle, one degree per frame, mask recomputed every frame",
+                            "saccade": "scripted saccades: 90 degrees along the cursor circle every 30 frames, mask "
+                                       "recomputed every frame"}[args.gaze_path],
                    "parallelism": parallelism,
                    "procedural_meshes": "box/bunny/earth stand-ins (the reference's .obj files are absent)"},
         "fps": round(K / elapsed, 2),
+        "fps_definition": "pipelined throughput: K frames enqueued back to back, frame N's reconstruction "
+                          "overlapping frame N+1's trace half (frames per second of the timed region); "
+                          "fps_serial is SURVEY §8(d)'s 1 / (wall time of one whole frame)",
         "frames_per_s_total": round(views * K / elapsed, 2),
+        "frame_ms_serial": serial,
+        "fps_serial": round(1e3 / serial["p50"], 2),
+        "frame_ms_serial_note": f"HIP events around one synchronised frame (update -> A-Trous, the two reconstruction "
+                                f"chains on their own streams), {n_timed} frames after 5 warm-ups, rank 0"
+                                + ("" if group is None else "; a group frame includes the exchange"),
+        "frame_clock_pipelined": clock,
+        "frame_clock_note": "every frame of the timed region: latency = from where its G-buffer may start (the "
+                            "gaze sample) to the end of its Sibson and A-Trous; interval = between consecutive "
+                            "frames' ends (what a display sees). HIP events, one context",
         "rays": {k: st[k] for k in ("gbuffer_primary", "primary", "shadow", "diffuse_bounce", "mirror",
                                     "refraction", "reflection", "truncated", "overflow")},
         "rays_note": "rank 0's counters over the timed frames",
@@ -466,11 +523,12 @@ def main():
     if group:
         group.destroy()
     # the GPU BVH builder on this scene (after every measurement: it replaces the BVH)
-    builds = [tracer.rebuild_bvh() for _ in range(5)]
-    result["bvh"] = {"builder": args.bvh, "gpu_rebuild_ms": round(float(np.median(builds[2:])), 3),
-                     "first_rebuild_ms": [round(b, 3) for b in builds[:2]],
-                     "note": "median of rebuilds 3-5; the first two include HIP's lazy loading of the builder's "
-                             "kernels (hipcub) into the process",
+    builds = [tracer.rebuild_bvh() for _ in range(6)]
+    result["bvh"] = {"builder": args.bvh, "gpu_rebuild_ms": round(float(np.median(builds)), 3),
+                     "max_rebuild_ms": round(float(max(builds)), 3),
+                     "rebuild_ms": [round(b, 3) for b in builds],
+                     "note": "fr_rebuild_bvh wall time of six rebuilds in a row (median, max and all); the context "
+                             "allocated and warmed the builder at fr_create",
                      "triangles": int(tracer.scene_arrays()["pos"].shape[0])}
     if rank == 0 and R == 1 and not args.no_cpu_baseline:
         try:
@@ -478,7 +536,10 @@ def main():
 
             def uni_fn(w, h):
                 return fovrt.Camera.preset(scene, w, h).uniforms(w, h)
-            result["cpu_baseline"] = cpu_baseline(args, arrays, uni_fn)
+            result["cpu_baseline"] = cpu_baseline(args, arrays, uni_fn, total_segs / K)
+            result["cpu_baseline"]["gpu_cpu_fps_ratio"] = {
+                "serial": round(result["fps_serial"] / result["cpu_baseline"]["fps"], 1),
+                "pipelined": round(result["fps"] / result["cpu_baseline"]["fps"], 1)}
         except Exception as e:  # report, never fake
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

@@ -155,6 +155,17 @@ void kt_harvest(fr_ctx* c, int i) {
   c->kt_frames++;
 }
 
+// One frame of the frame clock (fr_frame_clock): its latency, and its interval after the previous frame.
+void fc_harvest(fr_ctx* c, int i) {
+  hipEventSynchronize(c->fc_ev[i][1]);
+  float s = 0.0f, e = 0.0f;
+  hipEventElapsedTime(&s, c->fc_ref, c->fc_ev[i][0]);
+  hipEventElapsedTime(&e, c->fc_ref, c->fc_ev[i][1]);
+  c->fc_latency.push_back(e - s);
+  if (c->fc_prev_end >= 0.0) c->fc_interval.push_back((float)(e - c->fc_prev_end));
+  c->fc_prev_end = e;
+}
+
 float elapsed(hipEvent_t a, hipEvent_t b) {
   float ms = 0.0f;
   hipEventElapsedTime(&ms, a, b);
@@ -462,6 +473,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     c->err = "allocation (shard counts) failed";
     return bail(FR_E_NOMEM);
   }
+  memset(c->h_counts, 0, sizeof(uint32_t) * fr_ctx::MAX_SLOTS * FR_MAX_SHARD_RANKS);
   if (dalloc(&c->gclass, N) != hipSuccess || dalloc(&c->lp_cache, N) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
       dalloc(&c->counts, 4 * nblocks) != hipSuccess || dalloc(&c->offsets, 4 * nblocks) != hipSuccess ||
       dalloc(&c->tiles, 1024) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
@@ -541,6 +553,9 @@ int fr_destroy(fr_ctx* c) {
   for (auto e : c->ev_recon) if (e) hipEventDestroy(e);
   for (auto& q : c->kt_ev)
     for (auto e : q) if (e) hipEventDestroy(e);
+  for (auto& q : c->fc_ev)
+    for (auto e : q) if (e) hipEventDestroy(e);
+  if (c->fc_ref) hipEventDestroy(c->fc_ref);
   if (c->stream) hipStreamDestroy(c->stream);
   if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream3) hipStreamDestroy(c->stream3);
@@ -616,6 +631,14 @@ static int enqueue_geometry(fr_ctx* c, hipStream_t fs) {
     hipStreamWaitEvent(fs, c->ev_trace[sl], 0);
     c->trace_pending[sl] = false;
   }
+  if (c->fc_arm) {  // fr_frame_clock: where this frame's G-buffer (the first stage to read the gaze) may start
+    const int i = c->fc_next;
+    if (c->fc_pending == fr_ctx::FC_RING) { fc_harvest(c, i); c->fc_pending--; }
+    c->fc_cur = i;
+    c->fc_next = (i + 1) % fr_ctx::FC_RING;
+    c->fc_pending++;
+    hipEventRecord(c->fc_ev[i][0], fs);
+  }
   // frame = m_accumFrame++ ; a light change resets the counter afterwards (FR/PathTracer.cpp:99-116)
   c->U.frame = c->accum++;
   if (c->light_pending) { c->light_pending = false; c->accum = 0; }
@@ -652,6 +675,7 @@ static int enqueue_sampling(fr_ctx* c, hipStream_t fs) {
     hipMemcpyAsync(c->h_counts + (size_t)c->slot * FR_MAX_SHARD_RANKS, c->owner_counts_p[c->slot],
                    sizeof(uint32_t) * FR_MAX_SHARD_RANKS, hipMemcpyDeviceToHost, fs);
     hipEventRecord(c->ev_counts[c->slot], fs);
+    c->counts_valid[c->slot] = true;
   }
   c->compacted = false;
   return check_launch(c);
@@ -895,7 +919,10 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
       hipStreamWaitEvent(fs, c->ev[18], 0);
     }
     c->stream_dirty = false;
-    if ((rc = enqueue_geometry(c, fs))) return rc;
+    c->fc_arm = c->fc_on && recon;  // whole frames only (a group's trace half has no end of its own)
+    rc = enqueue_geometry(c, fs);
+    c->fc_arm = false;
+    if (rc) return rc;
     if (t) hipEventRecord(ev[1], c->stream);
     if ((rc = enqueue_sampling(c, fs))) return rc;
     if (t) hipEventRecord(ev[2], c->stream);
@@ -940,6 +967,10 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     hipStreamWaitEvent(c->stream3, ev[17], 0);
     hipEventRecord(c->ev_recon[c->slot], c->stream3);  // this slot's buffers are free again after this
     c->recon_pending[c->slot] = true;
+    if (c->fc_cur >= 0) {  // fr_frame_clock: both chains of this frame are done
+      hipEventRecord(c->fc_ev[c->fc_cur][1], c->stream3);
+      c->fc_cur = -1;
+    }
     if (t) join_recon(c);
   }
   if (t) {
@@ -1061,13 +1092,24 @@ int fr_set_shard_plan(fr_ctx* c, int rank, int count, int tile, const uint8_t* o
   hipSetDevice(c->cfg.device);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream5));
-  if (c->shard_map) { hipFree(c->shard_map); c->shard_map = nullptr; }
-  c->shard_owner.clear();
+  // the new map is complete before the old one goes: a failed allocation or copy leaves the previous
+  // plan (map, owners, uniforms) in force
+  uint32_t* new_map = nullptr;
   if (count > 1) {
-    HIP_TRY(c, hipMalloc((void**)&c->shard_map, nt * sizeof(uint32_t)));
-    HIP_TRY(c, hipMemcpy(c->shard_map, map.data(), nt * sizeof(uint32_t), hipMemcpyHostToDevice));
-    c->shard_owner.assign(owner, owner + nt);
+    if (hipMalloc((void**)&new_map, nt * sizeof(uint32_t)) != hipSuccess)
+      return fail(c, FR_E_NOMEM, "fr_set_shard_plan: device allocation failed, previous plan kept");
+    if (hipMemcpy(new_map, map.data(), nt * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+      hipFree(new_map);
+      return fail(c, FR_E_HIP, "fr_set_shard_plan: device copy failed, previous plan kept");
+    }
   }
+  if (c->shard_map) hipFree(c->shard_map);
+  c->shard_map = new_map;
+  c->shard_owner.clear();
+  if (count > 1) c->shard_owner.assign(owner, owner + nt);
+  // counts of the previous plan are stale (fr_shard_counts refuses until a front stage ran under this one)
+  for (bool& v : c->counts_valid) v = false;
+  memset(c->h_counts, 0, sizeof(uint32_t) * fr_ctx::MAX_SLOTS * FR_MAX_SHARD_RANKS);
   c->U.shard_rank = rank;
   c->U.shard_count = count;
   c->U.shard_tile = tile;
@@ -1138,6 +1180,8 @@ int fr_set_shard(fr_ctx* c, int rank, int count, int tile) { return fr_set_shard
 int fr_shard_counts(fr_ctx* c, uint32_t* counts, int n) {
   if (!c || !counts || n < 1) return FR_E_INVALID;
   if (c->U.shard_count <= 1) return fail(c, FR_E_STATE, "fr_shard_counts: call fr_set_shard with count > 1 first");
+  if (!c->counts_valid[c->slot])
+    return fail(c, FR_E_STATE, "fr_shard_counts: no front stage has run under the current shard plan");
   HIP_TRY(c, hipEventSynchronize(c->ev_counts[c->slot]));
   for (int r = 0; r < n; r++) counts[r] = r < c->U.shard_count ? c->h_counts[(size_t)c->slot * FR_MAX_SHARD_RANKS + r] : 0;
   return FR_OK;
@@ -1459,6 +1503,37 @@ int fr_kernel_timing(fr_ctx* c, int enable) {
   c->kt_next = c->kt_pending = 0;
   c->kt_frames = 0;
   c->kt_stage_ms = c->kt_kernel_ms = 0.0;
+  return FR_OK;
+}
+
+int fr_frame_clock(fr_ctx* c, int enable) {
+  if (!c) return FR_E_INVALID;
+  hipSetDevice(c->cfg.device);
+  if (enable && !c->fc_ref) {
+    HIP_TRY(c, hipEventCreate(&c->fc_ref));
+    for (auto& q : c->fc_ev)
+      for (auto& e : q) HIP_TRY(c, hipEventCreate(&e));
+  }
+  if (c->fc_pending) HIP_TRY(c, hipDeviceSynchronize());  // nothing recorded stays in flight across a reset
+  c->fc_on = enable != 0;
+  c->fc_next = c->fc_pending = 0;
+  c->fc_cur = -1;
+  c->fc_prev_end = -1.0;
+  c->fc_latency.clear();
+  c->fc_interval.clear();
+  if (c->fc_on) HIP_TRY(c, hipEventRecord(c->fc_ref, c->stream));
+  return FR_OK;
+}
+
+int fr_frame_clock_read(fr_ctx* c, float* latency_ms, float* interval_ms, int cap, int* n_latency, int* n_interval) {
+  if (!c || cap < 0 || (cap > 0 && (!latency_ms || !interval_ms)) || !n_latency || !n_interval) return FR_E_INVALID;
+  hipSetDevice(c->cfg.device);
+  for (; c->fc_pending > 0; c->fc_pending--)
+    fc_harvest(c, (c->fc_next - c->fc_pending + fr_ctx::FC_RING) % fr_ctx::FC_RING);
+  *n_latency = (int)std::min<size_t>(c->fc_latency.size(), (size_t)cap);
+  *n_interval = (int)std::min<size_t>(c->fc_interval.size(), (size_t)cap);
+  if (*n_latency) memcpy(latency_ms, c->fc_latency.data(), sizeof(float) * *n_latency);
+  if (*n_interval) memcpy(interval_ms, c->fc_interval.data(), sizeof(float) * *n_interval);
   return FR_OK;
 }
 

@@ -127,6 +127,7 @@ struct fr_ctx {
   uint32_t* owner_counts_p[MAX_SLOTS] = {};
   uint32_t* h_counts = nullptr;  // MAX_SLOTS x FR_MAX_SHARD_RANKS, pinned
   hipEvent_t ev_counts[MAX_SLOTS] = {};
+  bool counts_valid[MAX_SLOTS] = {};  // a front stage under the current plan recorded ev_counts[slot]
   // Tile-local front stages (fr_set_front_local): per 8x8 pixel tile, does this rank's sampling read
   // it (front_need, device; FrameUniforms::front_need while on); front_need_px = their pixel count.
   bool front_local = false;
@@ -206,6 +207,19 @@ struct fr_ctx {
   int kt_next = 0, kt_pending = 0;
   uint32_t kt_frames = 0;
   double kt_stage_ms = 0.0, kt_kernel_ms = 0.0;
+  // Frame clock of pipelined frames (fr_frame_clock): per frame, an event where its G-buffer may start
+  // (on the front stream, after the slot waits) and one after both reconstruction chains (stream3).
+  // latency = start -> end of one frame (gaze sample to finished image on the GPU), interval = end of
+  // the previous frame -> end of this one. Harvested like kt_ev.
+  static constexpr int FC_RING = 16;
+  hipEvent_t fc_ev[FC_RING][2] = {};
+  bool fc_on = false;
+  int fc_next = 0, fc_pending = 0;
+  hipEvent_t fc_ref = nullptr;  // recorded when the clock is enabled: every time is read against it
+  double fc_prev_end = -1.0;    // the previous harvested frame's end (ms after fc_ref)
+  int fc_cur = -1;              // the ring entry of the frame being enqueued
+  bool fc_arm = false;          // frame_half: this enqueue_geometry starts a whole frame
+  std::vector<float> fc_latency, fc_interval;
   // scene export copies
   std::vector<const float*> tex_ptrs;
   std::vector<int32_t> tex_dims, mat_pairs;

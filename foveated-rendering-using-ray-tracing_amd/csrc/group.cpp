@@ -224,6 +224,11 @@ int exchange(fr_group* g) {
     fr::launch_shard_pack_active(L.c->active, L.c->ray_count, n, L.c->img[L.c->hist_cache], vals, idx, L.c->stream);
     if (int rc = fri::check_launch(L.c)) return gfail(rc, fr_last_error(L.c));
     hipEventRecord(L.ev_packed, L.c->stream);
+    // The slot's active list and ray count are released to the front stages of frame + nslots (stream5
+    // waits for ev_trace[slot]) only once this pack has read them: enqueue_shading recorded ev_trace
+    // before the pack was queued, and the pack may still wait for frame - 2's transfers (ev_comm).
+    hipEventRecord(L.c->ev_trace[L.c->slot], L.c->stream);
+    L.c->trace_pending[L.c->slot] = true;
     if (g->comm) hipStreamWaitEvent(L.comm, L.ev_packed, 0);
   }
   // receive slabs of frame - 2 must have been unpacked

@@ -167,6 +167,9 @@ _SIGS = {
     "fr_reset_stats": [C.c_void_p],
     "fr_kernel_timing": [C.c_void_p, C.c_int],
     "fr_kernel_times": [C.c_void_p, C.POINTER(fr_stage_times)],
+    "fr_frame_clock": [C.c_void_p, C.c_int],
+    "fr_frame_clock_read": [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int),
+                            C.POINTER(C.c_int)],
     "fr_scene_export": [C.c_void_p, C.POINTER(fr_scene_arrays)],
     "fr_scene_create": [C.POINTER(fr_config), C.POINTER(C.c_void_p)],
     "fr_scene_get_arrays": [C.c_void_p, C.POINTER(fr_scene_arrays)],
@@ -476,6 +479,18 @@ class PathTracer:
         t = fr_stage_times()
         self._check(_lib.fr_kernel_times(self._ctx, C.byref(t)))
         return {"frames": t.frames, "shading_ms": t.shading_ms, "shade_paths_ms": t.shade_paths_ms}
+
+    def frame_clock(self, enable: bool):
+        """fr_frame_clock: starts (or stops and clears) the per-frame latency / interval events of fr_frame."""
+        self._check(_lib.fr_frame_clock(self._ctx, 1 if enable else 0))
+
+    def frame_clock_read(self, cap=100000):
+        """(latency_ms, interval_ms) numpy arrays of every frame since frame_clock(True)."""
+        lat = (C.c_float * cap)()
+        itv = (C.c_float * cap)()
+        nl, ni = C.c_int(0), C.c_int(0)
+        self._check(_lib.fr_frame_clock_read(self._ctx, lat, itv, cap, C.byref(nl), C.byref(ni)))
+        return (np.frombuffer(lat, np.float32, nl.value).copy(), np.frombuffer(itv, np.float32, ni.value).copy())
 
     def _frame(self, fn, timing):
         t = fr_frame_timing() if timing else None

@@ -392,6 +392,17 @@ typedef struct fr_stage_times {
 int fr_kernel_timing(fr_ctx* ctx, int enable);
 int fr_kernel_times(fr_ctx* ctx, fr_stage_times* out);
 
+/* Frame clock of fr_frame (no synchronisation added beyond a ring of 16 frames): after
+ * fr_frame_clock(ctx, 1) every fr_frame records a HIP event where its G-buffer may start (after the
+ * waits for its frame slot) and one after both of its reconstruction chains. fr_frame_clock_read
+ * returns, per frame since, the latency (start -> end: the gaze the frame samples to its finished
+ * Sibson and A-Trous images, on the GPU) and the interval between consecutive frames' ends (the frame
+ * time a display sees), in milliseconds; *n_latency / *n_interval receive the counts (at most cap each).
+ * The reference's frame time is the serial sum of its stage timers (FR/main.cpp:368-373).
+ * fr_frame_clock(ctx, 0) stops and clears. */
+int fr_frame_clock(fr_ctx* ctx, int enable);
+int fr_frame_clock_read(fr_ctx* ctx, float* latency_ms, float* interval_ms, int cap, int* n_latency, int* n_interval);
+
 /* Scene inspection (host copies owned by the context; valid until fr_destroy). */
 typedef struct fr_scene_arrays {
   int num_tris;

@@ -807,7 +807,7 @@ def test_composite_views_side_by_side(fovrt_mod):
     W, H = 96, 64
     eyes = [make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=1, dmd=1) for _ in range(2)]
     for k, t in enumerate(eyes):
-        cam = fovrt_mod.Camera.preset(1, W, H)
+        cam = fovrt_mod.Camera.preset(scene, W, H)
         cam.setPosition(np.asarray(cam.pos) + np.array([0.064 * (k - 0.5), 0, 0], np.float32))
         cam.lookAt(cam.target)
         t.update_optix_variables(cam)
@@ -909,10 +909,23 @@ GROUP_CASES = [  # (ranks, views, tile, split, moving, W, H, mask, jfa_ranks)
     (3, 1, 16, True, True, 160, 112, 4, 0), (4, 1, 128, True, False, 3840, 2160, 4, 0),
     (4, 1, 32, True, False, 200, 136, 4, 2), (6, 2, 32, True, True, 160, 112, 4, 2), (4, 1, 16, True, False, 200, 136, 0, 3),
     (8, 1, 128, True, False, 3840, 2160, 4, 0)]
+GROUP_SCENE = (1, 4, 3)  # bunny, 4 spp, diffuse_max_depth 3 (configs[2])
+# BASELINE.json configs[3] and [4] as their own group shapes (scene, spp, diffuse_max_depth appended):
+#   C4 vokselia 4K, 8 spp, saliency mask, one view tiled over 4 ranks;
+#   C5 vokselia 4K, 8 spp GI 3, saliency mask, two eyes of 4 ranks each with the stereo composite.
+# A still camera, so the tracers run the tile-local front with the saliency stencil's 4-px halo
+# (FR/cuda/samplingStep.cu:186-199); the two chains as FR/main.cpp:336-355.
+GROUP_CASES_CONFIGS = [
+    pytest.param(4, 1, 128, True, False, 3840, 2160, 0, 0, (2, 8, 1), id="C4-vokselia-4K-8spp-saliency-4ranks",
+                 marks=pytest.mark.timeout(600)),
+    pytest.param(8, 2, 128, True, False, 3840, 2160, 0, 0, (2, 8, 3), id="C5-vokselia-stereo-4K-8spp-gi3-2x4ranks",
+                 marks=pytest.mark.timeout(600)),
+]
 
 
-@pytest.mark.parametrize("R,V,tile,split,moving,W,H,mask,jfa", GROUP_CASES)
-def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving, W, H, mask, jfa):
+@pytest.mark.parametrize("R,V,tile,split,moving,W,H,mask,jfa,scn",
+                         [c + (GROUP_SCENE,) for c in GROUP_CASES] + GROUP_CASES_CONFIGS)
+def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving, W, H, mask, jfa, scn):
     """fr_group_frame over R in-process ranks (V views of G = R / V): pipelined frames (no host sync but
     each rank's own front stages); with moving=True the camera pans every frame and every rank receives
     every other rank's traced pixels. Each view's reconstruction ranks hold the single-context frame's
@@ -920,7 +933,8 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
     composite on rank 0 is the views' A-Trous images side by side."""
     import torch
     G = R // V
-    mk = lambda: make_tracer(fovrt_mod, W, H, scene=1, mask=mask, spp=4, dmd=3)
+    scene, spp, dmd = scn
+    mk = lambda: make_tracer(fovrt_mod, W, H, scene=scene, mask=mask, spp=spp, dmd=dmd)
     ranks = [mk() for _ in range(R)]
     fulls = [mk() for _ in range(V)]
     if G > 1:  # the group sums samples in fixed point (fr_group_config.sample_sum 2): the references too
@@ -928,7 +942,7 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
             f.set_sample_sum(2)
     cams = []
     for v in range(V):
-        cam = fovrt_mod.Camera.preset(1, W, H)
+        cam = fovrt_mod.Camera.preset(scene, W, H)
         cam.setPosition(np.asarray(cam.pos) + np.array([0.064 * (v - (V - 1) / 2), 0, 0], np.float32))
         cam.lookAt(cam.target)
         cams.append(cam)
@@ -1001,3 +1015,33 @@ def test_group_one_rank_rccl(fovrt_mod):
         assert equal_nan(t.read(tid), full.read(tid)), tid
     assert equal_nan(out.cpu().numpy().reshape(H, W, 4), full.read(TN.ATROUS))
     g.destroy()
+
+
+def test_frame_clock_and_shard_count_state(fovrt_mod):
+    """fr_frame_clock: one latency per pipelined frame and one interval per pair of consecutive frames,
+    all positive, the latency at least the serial frame's G-buffer-to-A-Trous span's order; more frames
+    than the event ring (16) are harvested in order. fr_shard_counts refuses before a front stage has run
+    under the current shard plan (no stale or uninitialised counts), and answers after one."""
+    W, H = 128, 96
+    t = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    t.frame_clock(True)
+    for _ in range(40):
+        t.frame(timing=False)
+    lat, itv = t.frame_clock_read()
+    assert lat.size == 40 and itv.size == 39
+    assert (lat > 0).all() and (itv > 0).all() and np.isfinite(lat).all()
+    t.frame_clock(False)
+    lat, itv = t.frame_clock_read()
+    assert lat.size == 0 and itv.size == 0
+    t.set_shard(0, 2, 32)
+    with pytest.raises(fovrt_mod.FovrtError) as e:
+        t.shard_counts(2)
+    assert e.value.code == fovrt_mod.FR_E_STATE
+    t.frame(timing=False)
+    t.synchronize()
+    n = t.shard_counts(2)
+    assert int(n[0]) == int(t.read(TN.MASK).sum()) and int(n[1]) > 0  # rank 0's own tiles are its mask
+    t.set_shard(0, 3, 32)  # a new plan: the counts of the old one are gone
+    with pytest.raises(fovrt_mod.FovrtError):
+        t.shard_counts(3)
+    t.destroy()
