@@ -307,6 +307,51 @@ static int gpu_rebuild(fr_ctx* c) {
   return FR_OK;
 }
 
+// The densest exact storage of a host texture (DevTexture): FR_TEX_UNORM8 when every channel of every
+// texel is (float)b / 255.0f, FR_TEX_RGBE when every texel is m * 2^(e - 136) with alpha 1 (load_hdr's
+// decoding), else FR_TEX_F32. Each candidate is decoded back here with the loaders' own formulas and
+// must reproduce every float bit for bit.
+static int pack_texture(const HostTexture& t, std::vector<uint32_t>& out) {
+  const size_t n = t.data.size();
+  auto same = [](float a, float b) { return std::memcmp(&a, &b, sizeof(float)) == 0; };
+  out.resize(n);
+  bool unorm = true;
+  for (size_t i = 0; i < n && unorm; i++) {
+    const float v[4] = {t.data[i].x, t.data[i].y, t.data[i].z, t.data[i].w};
+    uint32_t word = 0;
+    for (int c = 0; c < 4; c++) {
+      const long b = std::lrint((double)v[c] * 255.0);
+      if (b < 0 || b > 255 || !same((float)b / 255.0f, v[c])) { unorm = false; break; }
+      word |= (uint32_t)b << (8 * c);
+    }
+    out[i] = word;
+  }
+  if (unorm) return FR_TEX_UNORM8;
+  for (size_t i = 0; i < n; i++) {
+    const float v[3] = {t.data[i].x, t.data[i].y, t.data[i].z};
+    if (!same(t.data[i].w, 1.0f)) return FR_TEX_F32;
+    const float M = std::max(v[0], std::max(v[1], v[2]));
+    uint32_t word = 0;
+    if (M > 0.0f) {
+      int ex = 0;
+      std::frexp(M, &ex);
+      const int k = ex - 8, e = k + 136;  // M / 2^k in [128, 256)
+      if (e < 1 || e > 255) return FR_TEX_F32;
+      const float f = std::ldexp(1.0f, e - 136);
+      for (int c = 0; c < 3; c++) {
+        const float m = std::ldexp(v[c], -k);
+        if (!(m >= 0.0f && m <= 255.0f) || m != std::floor(m) || !same((float)(int)m * f, v[c])) return FR_TEX_F32;
+        word |= (uint32_t)m << (8 * c);
+      }
+      word |= (uint32_t)e << 24;
+    } else if (!(same(v[0], 0.0f) && same(v[1], 0.0f) && same(v[2], 0.0f))) {
+      return FR_TEX_F32;
+    }
+    out[i] = word;
+  }
+  return FR_TEX_RGBE;
+}
+
 int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (!out) return fail(nullptr, FR_E_INVALID, "out is NULL");
   *out = nullptr;
@@ -362,6 +407,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (const char* v = getenv("FOVRT_SHADE_CHUNK_REFR")) c->chunk_refr = (uint32_t)std::max(0, atoi(v));
   if (const char* v = getenv("FOVRT_SHADE_XCD_BANDS")) c->xcd_bands = atoi(v) != 0;
   if (const char* v = getenv("FOVRT_SHADE_HANDOFF")) c->handoff = (uint32_t)std::min(std::max(atoi(v), 0), 2);
+  if (const char* v = getenv("FOVRT_TEX_PACKING")) c->tex_packing = atoi(v) != 0;  // A/B knob: 0 = RGBA32F textures
   {  // FOVRT_SLOTS: frame slots of the pipelined loop (2 or 3; A/B knob)
     const char* v = getenv("FOVRT_SLOTS");
     if (v) c->nslots = std::max(2, std::min(fr_ctx::MAX_SLOTS, atoi(v)));
@@ -435,8 +481,20 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   c->d_tex.resize(s.texs.size(), nullptr);
   std::vector<DevTexture> htex(s.texs.size());
   for (size_t i = 0; i < s.texs.size(); i++) {
-    if (!up(&c->d_tex[i], s.texs[i].data)) { c->err = "device allocation (texture) failed"; return bail(FR_E_NOMEM); }
-    htex[i] = DevTexture{c->d_tex[i], s.texs[i].w, s.texs[i].h};
+    std::vector<uint32_t> packed;
+    const int kind = c->tex_packing ? pack_texture(s.texs[i], packed) : FR_TEX_F32;
+    htex[i] = DevTexture{nullptr, nullptr, s.texs[i].w, s.texs[i].h, kind};
+    if (kind == FR_TEX_F32) {
+      f4* p = nullptr;
+      if (!up(&p, s.texs[i].data)) { c->err = "device allocation (texture) failed"; return bail(FR_E_NOMEM); }
+      c->d_tex[i] = p;
+      htex[i].data = p;
+    } else {
+      uint32_t* p = nullptr;
+      if (!up(&p, packed)) { c->err = "device allocation (texture) failed"; return bail(FR_E_NOMEM); }
+      c->d_tex[i] = p;
+      htex[i].packed = p;
+    }
   }
   if (!up(&c->d_mats, s.mats) || !up(&c->d_texs, htex)) { c->err = "device allocation (materials) failed"; return bail(FR_E_NOMEM); }
   d.mats = c->d_mats;
@@ -1493,6 +1551,20 @@ int fr_get_stats(fr_ctx* c, fr_stats* s) {
 
 // Test hook (not part of include/fovrt.h): the host build of the bound JFA and Sibson use.
 float fr__sqrt_le_bound(float s) { return sqrt_le_bound(s); }
+
+// Test hook (not part of include/fovrt.h): pack_texture on n RGBA32F texels; returns the FR_TEX_* kind
+// and writes the packed words (n of them) for the packed kinds.
+int fr__pack_texture(const float* rgba, int n, uint32_t* out) {
+  if (!rgba || n < 0 || !out) return -1;
+  HostTexture t;
+  t.w = n; t.h = 1;
+  t.data.resize((size_t)n);
+  memcpy(t.data.data(), rgba, sizeof(f4) * (size_t)n);
+  std::vector<uint32_t> packed;
+  const int kind = pack_texture(t, packed);
+  if (kind != FR_TEX_F32) memcpy(out, packed.data(), sizeof(uint32_t) * (size_t)n);
+  return kind;
+}
 
 int fr_kernel_timing(fr_ctx* c, int enable) {
   if (!c) return FR_E_INVALID;

@@ -154,7 +154,8 @@ struct fr_ctx {
   fr::BvhWork* bvh_work = nullptr;
   bool tree_full_cap = false;  // d_nodes / d_tri / d_prim hold one entry per triangle (a device-built tree)
   TriShade* d_shade = nullptr;
-  std::vector<f4*> d_tex;
+  std::vector<void*> d_tex;
+  bool tex_packing = true;  // textures in their densest exact storage (pack_texture); FOVRT_TEX_PACKING=0: RGBA32F
   DevMaterial* d_mats = nullptr;
   DevTexture* d_texs = nullptr;
   DevScene dsc;

@@ -43,9 +43,17 @@ struct alignas(16) TriShade {
 #define FR_SHADE_HAS_NORMALS 0x100
 #define FR_SHADE_HAS_UV 0x200
 
+// Texel storage, the densest exact form per texture (context.cpp, pack_texture): RGBA32F; RGBA8 when
+// every channel is exactly b / 255.0f (the 8-bit PPM / PNG textures sutil::loadTexture reads as
+// normalised bytes); RGBE when every texel is (m * 2^(e - 136), alpha 1) (the Radiance .hdr environment
+// map, FR/PathTracer.cpp:454-455). Decoding is exact (tex_texel, k_trace.hip): a lookup returns the
+// RGBA32F texel bit for bit, from a quarter of the bytes.
+enum { FR_TEX_F32 = 0, FR_TEX_UNORM8 = 1, FR_TEX_RGBE = 2 };
 struct DevTexture {
-  const f4* data;  // row 0 = bottom (v = 0), RGBA, normalised float
+  const f4* data;          // FR_TEX_F32: row 0 = bottom (v = 0), RGBA, normalised float
+  const uint32_t* packed;  // FR_TEX_UNORM8 / FR_TEX_RGBE: r | g << 8 | b << 16 | (a or e) << 24
   int32_t w, h;
+  int32_t kind;
 };
 
 struct DevMaterial {

@@ -185,6 +185,16 @@ class PathTracer {
   // live per-launch HIP-event timing of the shading stage (off by default)
   void kernel_timing(bool on) { check(fr_kernel_timing(ctx(), on ? 1 : 0), ctx_, "kernel_timing"); }
   fr_stage_times kernel_times() { fr_stage_times t{}; check(fr_kernel_times(ctx(), &t), ctx_, "kernel_times"); return t; }
+  // per-frame latency and display interval of pipelined frames (fr_frame_clock), in ms
+  void frame_clock(bool on) { check(fr_frame_clock(ctx(), on ? 1 : 0), ctx_, "frame_clock"); }
+  void frame_clock_read(std::vector<float>& latency_ms, std::vector<float>& interval_ms, int cap = 65536) {
+    latency_ms.resize((size_t)cap);
+    interval_ms.resize((size_t)cap);
+    int nl = 0, ni = 0;
+    check(fr_frame_clock_read(ctx(), latency_ms.data(), interval_ms.data(), cap, &nl, &ni), ctx_, "frame_clock_read");
+    latency_ms.resize((size_t)nl);
+    interval_ms.resize((size_t)ni);
+  }
   fr_ctx* ctx() const {
     if (!ctx_) throw Error(FR_E_STATE, "PathTracer used before initialize()");
     return ctx_;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Sibson alone and the JFA disc radii per gaze position of bench.py --gaze-path's cursor circle (4K
 bunny, signed log-polar mask): what sets the eye-tracked frame's Sibson time. Usage:
-python scripts/gaze_probe.py"""
+python scripts/gaze_probe.py [angle ...] (default: centred, 0, 1, 2, 45, 90, 180)"""
 import os
 import sys
 import numpy as np
@@ -17,7 +17,8 @@ TN = fovrt.TextureName
 si = fovrt.SibsonInterpolation(t)
 yy, xx = np.mgrid[0:H, 0:W]
 fx, fy = (xx + 0.5) / W, (yy + 0.5) / H
-for ang in [None, 0, 1, 2, 45, 90, 180]:
+angles = [None if a == "c" else float(a) for a in sys.argv[1:]] or [None, 0, 1, 2, 45, 90, 180]
+for ang in angles:
     if ang is None:
         t.reset_gaze()
     else:
