@@ -408,6 +408,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (const char* v = getenv("FOVRT_SHADE_XCD_BANDS")) c->xcd_bands = atoi(v) != 0;
   if (const char* v = getenv("FOVRT_SHADE_HANDOFF")) c->handoff = (uint32_t)std::min(std::max(atoi(v), 0), 2);
   if (const char* v = getenv("FOVRT_TEX_PACKING")) c->tex_packing = atoi(v) != 0;  // A/B knob: 0 = RGBA32F textures
+  if (const char* v = getenv("FOVRT_SIB_STRIP")) c->sib_strip = atoi(v) != 0;      // A/B knob: 1 = the strip kernel
   {  // FOVRT_SLOTS: frame slots of the pipelined loop (2 or 3; A/B knob)
     const char* v = getenv("FOVRT_SLOTS");
     if (v) c->nslots = std::max(2, std::min(fr_ctx::MAX_SLOTS, atoi(v)));
@@ -543,7 +544,9 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       hipMalloc((void**)&c->item_store, shade_item_store_f4() * sizeof(f4)) != hipSuccess ||
       (cfg.sibson_mode == 0 && (dalloc(&c->sib_prefix, (size_t)(c->W + 1) * c->H) != hipSuccess ||
                                 dalloc(&c->sib_blocks, (size_t)sibson_prefix_blocks(c->W) * c->H) != hipSuccess ||
-                                hipMalloc((void**)&c->sib_wide, ((size_t)c->W * c->H + 2) * sizeof(uint32_t)) != hipSuccess))) {
+                                hipMalloc((void**)&c->sib_wide, ((size_t)c->W * c->H + 2) * sizeof(uint32_t)) != hipSuccess ||
+                                hipMalloc((void**)&c->sib_strips, sibson_strip_words(c->W, c->H) * sizeof(uint32_t)) != hipSuccess ||
+                                dalloc(&c->sib_tt, sibson_tt_texels(c->W, c->H)) != hipSuccess))) {
     c->err = "device allocation (work buffers) failed";
     return bail(FR_E_NOMEM);
   }
@@ -604,7 +607,7 @@ int fr_destroy(fr_ctx* c) {
   if (c->h_counts) hipHostFree(c->h_counts);
   for (auto e : c->ev_counts) if (e) hipEventDestroy(e);
   fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->item_store); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
-  fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks); fr(c->sib_wide);
+  fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks); fr(c->sib_wide); fr(c->sib_strips); fr(c->sib_tt);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->ev_front) hipEventDestroy(c->ev_front);
   for (auto e : c->ev_trace) if (e) hipEventDestroy(e);
@@ -835,8 +838,9 @@ static int enqueue_sibson(fr_ctx* c, hipStream_t stream = nullptr) {
   if (c->cfg.sibson_mode == 1)  // per tap, bit-exact against the oracle
     launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, stream ? stream : c->stream);
   else  // run form (default): exact tap sets, rounding-level differences
-    launch_sibson_runs(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->sib_prefix, c->sib_blocks, c->sib_wide,
-                       c->img[P_SIBSON], c->W, c->H, c->sib_prefix_fresh, stream ? stream : c->stream);
+    launch_sibson_runs(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->sib_prefix, c->sib_blocks, c->sib_tt, c->sib_wide,
+                       c->sib_strips, c->img[P_SIBSON], c->W, c->H, c->sib_prefix_fresh, c->sib_strip,
+                       stream ? stream : c->stream);
   return check_launch(c);
 }
 static int enqueue_pullpush(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {

@@ -41,8 +41,10 @@ void launch_shard_pack_active(const uint32_t*, const uint32_t*, uint32_t, const 
 void launch_shard_unpack_active(const f4*, const uint32_t*, uint32_t, uint32_t, f4*, f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, f4*, f4*, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
-void launch_sibson_runs(const f4*, const f4*, f4*, f4*, uint32_t*, f4*, int, int, bool, hipStream_t);
+void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, uint32_t*, uint32_t*, f4*, int, int, bool, bool, hipStream_t);
 int sibson_prefix_blocks(int W);
+size_t sibson_strip_words(int W, int H);
+size_t sibson_tt_texels(int W, int H);
 struct BvhWork;
 bool gpu_build_bvh(BvhWork**, const f3*, int, BvhNode*, TriGeo*, int32_t*, int*, int*, int*, hipStream_t, std::string&);
 void bvh_work_free(BvhWork*);
@@ -156,6 +158,7 @@ struct fr_ctx {
   TriShade* d_shade = nullptr;
   std::vector<void*> d_tex;
   bool tex_packing = true;  // textures in their densest exact storage (pack_texture); FOVRT_TEX_PACKING=0: RGBA32F
+  bool sib_strip = false;   // Sibson's big discs by k_sibson_strip (FOVRT_SIB_STRIP=1); default: k_sibson_runs / k_sibson_wide
   DevMaterial* d_mats = nullptr;
   DevTexture* d_texs = nullptr;
   DevScene dsc;
@@ -189,6 +192,8 @@ struct fr_ctx {
   f4 *pull = nullptr, *push = nullptr, *snap = nullptr;
   f4 *sib_prefix = nullptr, *sib_blocks = nullptr;  // Sibson run form: per-row block prefix sums + block totals
   uint32_t* sib_wide = nullptr;  // Sibson run form: wide-disc pixel lists (two counts, then W*H indices)
+  uint32_t* sib_strips = nullptr;  // Sibson run form: k_sibson_strip's strip list and flags (sibson_strip_words)
+  f4* sib_tt = nullptr;            // Sibson run form: per-row prefix of the block totals (sibson_tt_texels)
   bool sib_prefix_fresh = false;  // the last JFA wrote them with JFA_COLOR (cleared when JFA_COLOR is written)
   int pp_S = 0;
   DevStats* stats = nullptr;
