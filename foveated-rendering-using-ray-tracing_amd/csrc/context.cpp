@@ -1556,6 +1556,17 @@ int fr_get_stats(fr_ctx* c, fr_stats* s) {
 // Test hook (not part of include/fovrt.h): the host build of the bound JFA and Sibson use.
 float fr__sqrt_le_bound(float s) { return sqrt_le_bound(s); }
 
+// Diagnostic hook (not part of include/fovrt.h): the last Sibson pass's list counts: strips (k_sibson_strip),
+// wide[0] and wide[1] (k_sibson_wide's two lists).
+int fr__sibson_counts(fr_ctx* c, uint32_t* out3) {
+  if (!c || !out3 || !c->sib_strips) return FR_E_INVALID;
+  hipSetDevice(c->cfg.device);
+  HIP_TRY(c, hipDeviceSynchronize());
+  HIP_TRY(c, hipMemcpy(out3, c->sib_strips, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(out3 + 1, c->sib_wide, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return FR_OK;
+}
+
 // Test hook (not part of include/fovrt.h): pack_texture on n RGBA32F texels; returns the FR_TEX_* kind
 // and writes the packed words (n of them) for the packed kinds.
 int fr__pack_texture(const float* rgba, int n, uint32_t* out) {

@@ -27,6 +27,10 @@ yy, xx = np.mgrid[0:H, 0:W]
 d = np.hypot(coord[..., 0] - (xx + 0.5) / W, coord[..., 1] - (yy + 0.5) / H) * H
 si = fovrt.SibsonInterpolation(t)
 ms = [si.render() / 1e6 for _ in range(K)]
+import ctypes as C
+cnt = (C.c_uint32 * 3)()
+fovrt.load_library().fr__sibson_counts(t._ctx, cnt)
+print(f"lists: strips {cnt[0]}, wide[0] {cnt[1]}, wide[1] {cnt[2]}")
 big = d > 64
 strips = int(np.any(big.reshape(H, -1, 64) if W % 64 == 0 else big, axis=-1).sum())
 print(f"mask density {mask.mean():.4f}; disc half-rows mean {d.mean():.1f} max {d.max():.1f}; big pixels "
