@@ -408,7 +408,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (const char* v = getenv("FOVRT_SHADE_XCD_BANDS")) c->xcd_bands = atoi(v) != 0;
   if (const char* v = getenv("FOVRT_SHADE_HANDOFF")) c->handoff = (uint32_t)std::min(std::max(atoi(v), 0), 2);
   if (const char* v = getenv("FOVRT_TEX_PACKING")) c->tex_packing = atoi(v) != 0;  // A/B knob: 0 = RGBA32F textures
-  if (const char* v = getenv("FOVRT_SIB_STRIP")) c->sib_strip = atoi(v) != 0;      // A/B knob: 1 = the strip kernel
+  if (const char* v = getenv("FOVRT_SIB_STRIP")) c->sib_strip = atoi(v) != 0;      // A/B knob: 0 = k_sibson_wide for the big discs
   {  // FOVRT_SLOTS: frame slots of the pipelined loop (2 or 3; A/B knob)
     const char* v = getenv("FOVRT_SLOTS");
     if (v) c->nslots = std::max(2, std::min(fr_ctx::MAX_SLOTS, atoi(v)));

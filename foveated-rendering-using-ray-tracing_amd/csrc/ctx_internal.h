@@ -158,7 +158,7 @@ struct fr_ctx {
   TriShade* d_shade = nullptr;
   std::vector<void*> d_tex;
   bool tex_packing = true;  // textures in their densest exact storage (pack_texture); FOVRT_TEX_PACKING=0: RGBA32F
-  bool sib_strip = false;   // Sibson's big discs by k_sibson_strip (FOVRT_SIB_STRIP=1); default: k_sibson_runs / k_sibson_wide
+  bool sib_strip = true;    // Sibson's big discs by k_sibson_strip (default; FOVRT_SIB_STRIP=0: k_sibson_wide)
   DevMaterial* d_mats = nullptr;
   DevTexture* d_texs = nullptr;
   DevScene dsc;

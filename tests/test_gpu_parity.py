@@ -397,8 +397,9 @@ def test_sibson_run_form_offcentre_gaze_4k(fovrt_mod):
     """The 4K log-polar mask of bench.py --gaze-path's cursor at 180 degrees (gaze (1380, 1080)) leaves
     holes whose discs reach ~1,100 rows: the widest pixels (k_sibson_wide) and a sample of the rest
     against the shader's per-pixel loops. The seeds are the mask alone (no carried history), so the
-    holes are wider than in the bench's frames (mean disc 103 rows): the pass took ~96 ms here with
-    k_sibson_wide; the bound is a regression guard against the per-lane tap walk (O(d^2) per pixel)."""
+    holes are wider than in the bench's frames (mean disc 103 rows): the pass takes ~28 ms here with
+    k_sibson_strip (41 ms with k_sibson_wide alone, FOVRT_SIB_STRIP=0; ~96 ms before the border runs' split,
+    round 4); the bound is a regression guard against per-tap walks."""
     W, H = 3840, 2160
     mask = logpolar_mask_np(W, H, 1380, 1080, signed=True)
     img = sparse_image(W, H, mask, seed=11)
@@ -418,7 +419,7 @@ def test_sibson_run_form_offcentre_gaze_4k(fovrt_mod):
             continue
         assert sf[y, x, 3] == 1.0, (x, y)
         assert np.abs(sf[y, x, :3] - ref).max() <= SIB_RUN_MAX, (x, y, d[y, x] * H, sf[y, x, :3], ref)
-    assert ns / 1e6 < 250.0, ns / 1e6
+    assert ns / 1e6 < 80.0, ns / 1e6
 
 
 @pytest.mark.parametrize("W,H", [(64, 64), (96, 64), (256, 256), (130, 70)])
