@@ -546,7 +546,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
                                 dalloc(&c->sib_blocks, (size_t)sibson_prefix_blocks(c->W) * c->H) != hipSuccess ||
                                 hipMalloc((void**)&c->sib_wide, ((size_t)c->W * c->H + 2) * sizeof(uint32_t)) != hipSuccess ||
                                 hipMalloc((void**)&c->sib_strips, sibson_strip_words(c->W, c->H) * sizeof(uint32_t)) != hipSuccess ||
-                                dalloc(&c->sib_tt, sibson_tt_texels(c->W, c->H)) != hipSuccess))) {
+                                dalloc(&c->sib_rowp, sibson_rowp_texels(c->W, c->H)) != hipSuccess))) {
     c->err = "device allocation (work buffers) failed";
     return bail(FR_E_NOMEM);
   }
@@ -607,7 +607,7 @@ int fr_destroy(fr_ctx* c) {
   if (c->h_counts) hipHostFree(c->h_counts);
   for (auto e : c->ev_counts) if (e) hipEventDestroy(e);
   fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->item_store); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
-  fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks); fr(c->sib_wide); fr(c->sib_strips); fr(c->sib_tt);
+  fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks); fr(c->sib_wide); fr(c->sib_strips); fr(c->sib_rowp);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->ev_front) hipEventDestroy(c->ev_front);
   for (auto e : c->ev_trace) if (e) hipEventDestroy(e);
@@ -838,7 +838,7 @@ static int enqueue_sibson(fr_ctx* c, hipStream_t stream = nullptr) {
   if (c->cfg.sibson_mode == 1)  // per tap, bit-exact against the oracle
     launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, stream ? stream : c->stream);
   else  // run form (default): exact tap sets, rounding-level differences
-    launch_sibson_runs(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->sib_prefix, c->sib_blocks, c->sib_tt, c->sib_wide,
+    launch_sibson_runs(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->sib_prefix, c->sib_blocks, c->sib_rowp, c->sib_wide,
                        c->sib_strips, c->img[P_SIBSON], c->W, c->H, c->sib_prefix_fresh, c->sib_strip,
                        stream ? stream : c->stream);
   return check_launch(c);

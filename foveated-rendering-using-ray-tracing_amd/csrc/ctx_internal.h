@@ -44,7 +44,7 @@ void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
 void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, uint32_t*, uint32_t*, f4*, int, int, bool, bool, hipStream_t);
 int sibson_prefix_blocks(int W);
 size_t sibson_strip_words(int W, int H);
-size_t sibson_tt_texels(int W, int H);
+size_t sibson_rowp_texels(int W, int H);
 struct BvhWork;
 bool gpu_build_bvh(BvhWork**, const f3*, int, BvhNode*, TriGeo*, int32_t*, int*, int*, int*, hipStream_t, std::string&);
 void bvh_work_free(BvhWork*);
@@ -193,7 +193,7 @@ struct fr_ctx {
   f4 *sib_prefix = nullptr, *sib_blocks = nullptr;  // Sibson run form: per-row block prefix sums + block totals
   uint32_t* sib_wide = nullptr;  // Sibson run form: wide-disc pixel lists (two counts, then W*H indices)
   uint32_t* sib_strips = nullptr;  // Sibson run form: k_sibson_strip's strip list and flags (sibson_strip_words)
-  f4* sib_tt = nullptr;            // Sibson run form: per-row prefix of the block totals (sibson_tt_texels)
+  f4* sib_rowp = nullptr;          // Sibson strip kernel: whole-row prefix sums (sibson_rowp_texels)
   bool sib_prefix_fresh = false;  // the last JFA wrote them with JFA_COLOR (cleared when JFA_COLOR is written)
   int pp_S = 0;
   DevStats* stats = nullptr;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Sibson A/B (k_sibson_strip with whole-row prefixes vs k_sibson_wide), the strip kernel's counters, and the
+# stages' kernels alone with the JFA steps in XCD order and in round-robin order.
+set -o pipefail
+mkdir -p gpurun_out
+bash scripts/r04_ab4.sh > gpurun_out/ab4.log 2>&1 || { tail -30 gpurun_out/ab4.log; exit 1; }
+tail -12 gpurun_out/ab4.log
+bash scripts/pmc_sibstrip.sh 1 || exit 2
+FOVRT_JFA_XCD=0 bash scripts/stage_kernels.sh stagek_xcd0 > gpurun_out/stagek_xcd0.txt || exit 3
+FOVRT_JFA_XCD=1 bash scripts/stage_kernels.sh stagek_xcd1 > gpurun_out/stagek_xcd1.txt || exit 4
+grep -h "jfa\|geometry=" gpurun_out/stagek_xcd0.txt gpurun_out/stagek_xcd0/out.txt gpurun_out/stagek_xcd1.txt gpurun_out/stagek_xcd1/out.txt
