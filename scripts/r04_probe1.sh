@@ -5,7 +5,10 @@ set -o pipefail
 mkdir -p gpurun_out
 bash scripts/r04_ab4.sh > gpurun_out/ab4.log 2>&1 || { tail -30 gpurun_out/ab4.log; exit 1; }
 tail -12 gpurun_out/ab4.log
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "jfa or JFA or jump or Jump" > gpurun_out/jfa_tests.log 2>&1 || { tail -30 gpurun_out/jfa_tests.log; exit 5; }
+tail -1 gpurun_out/jfa_tests.log
 bash scripts/pmc_sibstrip.sh 1 || exit 2
 FOVRT_JFA_XCD=0 bash scripts/stage_kernels.sh stagek_xcd0 > gpurun_out/stagek_xcd0.txt || exit 3
 FOVRT_JFA_XCD=1 bash scripts/stage_kernels.sh stagek_xcd1 > gpurun_out/stagek_xcd1.txt || exit 4
-grep -h "jfa\|geometry=" gpurun_out/stagek_xcd0.txt gpurun_out/stagek_xcd0/out.txt gpurun_out/stagek_xcd1.txt gpurun_out/stagek_xcd1/out.txt
+FOVRT_JFA_FUSE_INIT=0 bash scripts/stage_kernels.sh stagek_nofuse > gpurun_out/stagek_nofuse.txt || exit 6
+for t in xcd0 xcd1 nofuse; do echo "== $t"; grep -h "jfa\|sibson\|geometry=" gpurun_out/stagek_$t.txt gpurun_out/stagek_$t/out.txt; done
