@@ -10,5 +10,4 @@ tail -1 gpurun_out/jfa_tests.log
 bash scripts/pmc_sibstrip.sh 1 || exit 2
 FOVRT_JFA_XCD=0 bash scripts/stage_kernels.sh stagek_xcd0 > gpurun_out/stagek_xcd0.txt || exit 3
 FOVRT_JFA_XCD=1 bash scripts/stage_kernels.sh stagek_xcd1 > gpurun_out/stagek_xcd1.txt || exit 4
-FOVRT_JFA_FUSE_INIT=0 bash scripts/stage_kernels.sh stagek_nofuse > gpurun_out/stagek_nofuse.txt || exit 6
-for t in xcd0 xcd1 nofuse; do echo "== $t"; grep -h "jfa\|sibson\|geometry=" gpurun_out/stagek_$t.txt gpurun_out/stagek_$t/out.txt; done
+for t in xcd0 xcd1; do echo "== $t"; grep -h "jfa\|sibson\|geometry=" gpurun_out/stagek_$t.txt gpurun_out/stagek_$t/out.txt; done
