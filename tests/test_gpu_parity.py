@@ -808,7 +808,7 @@ def test_composite_views_side_by_side(fovrt_mod):
     W, H = 96, 64
     eyes = [make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=1, dmd=1) for _ in range(2)]
     for k, t in enumerate(eyes):
-        cam = fovrt_mod.Camera.preset(scene, W, H)
+        cam = fovrt_mod.Camera.preset(1, W, H)
         cam.setPosition(np.asarray(cam.pos) + np.array([0.064 * (k - 0.5), 0, 0], np.float32))
         cam.lookAt(cam.target)
         t.update_optix_variables(cam)
