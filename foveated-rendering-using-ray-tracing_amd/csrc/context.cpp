@@ -603,7 +603,7 @@ int fr_destroy(fr_ctx* c) {
   fr(c->d_mats); fr(c->d_texs);
   for (auto p : c->img) fr(p);
   for (int k = 0; k < fr_ctx::MAX_SLOTS; k++) { fr(c->mask_p[k]); fr(c->ray_count_p[k]); fr(c->active_p[k]); fr(c->owner_counts_p[k]); }
-  fr(c->bcount); fr(c->shard_map); fr(c->front_need);
+  fr(c->bcount); fr(c->shard_map); fr(c->front_need); fr(c->shade_radiance);
   if (c->h_counts) hipHostFree(c->h_counts);
   for (auto e : c->ev_counts) if (e) hipEventDestroy(e);
   fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->item_store); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
@@ -789,7 +789,8 @@ static int enqueue_shading(fr_ctx* c) {
   if (kt) hipEventRecord(kt[2], c->stream);
   hipStreamWaitEvent(c->stream, c->ev[12], 0);
   launch_shade_resolve(c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache], c->samples,
-                       c->sample_help, c->img[c->hist_cur], c->img[P_shd(c)], c->shade_ctr, c->handoff, c->stream);
+                       c->sample_help, c->img[c->hist_cur], c->img[P_shd(c)], c->shade_ctr, c->handoff,
+                       c->U.shard_count > 1 ? c->shade_radiance : nullptr, c->stream);
   if (kt) hipEventRecord(kt[3], c->stream);
   // this slot's WEIGHT / mask / active list are free for the front stages of frame + nslots after this
   hipEventRecord(c->ev_trace[c->slot], c->stream);
@@ -1087,8 +1088,8 @@ int fr_shard_unpack_active_enqueue(fr_ctx* c, const void* slab, size_t slab_byte
   hipSetDevice(c->cfg.device);
   const f4* vals = (const f4*)slab;
   const uint32_t* idx = (const uint32_t*)((const char*)slab + (size_t)capacity * sizeof(f4));
-  launch_shard_unpack_active(vals, idx, count, (uint32_t)((size_t)c->W * c->H), c->img[c->hist_cache], c->img[P_shd(c)],
-                             c->stream);
+  launch_shard_unpack_active(c->U, vals, idx, count, (uint32_t)((size_t)c->W * c->H), c->img[P_wgt(c)],
+                             c->img[c->hist_cur], c->img[c->hist_cache], c->img[P_shd(c)], c->stream);
   return check_launch(c);
 }
 
@@ -1158,6 +1159,11 @@ int fr_set_shard_plan(fr_ctx* c, int rank, int count, int tile, const uint8_t* o
   // plan (map, owners, uniforms) in force
   uint32_t* new_map = nullptr;
   if (count > 1) {
+    // a sharded rank's traced radiance (k_shade_resolve, active order): what it sends (fr_shard_pack_active)
+    if (!c->shade_radiance && dalloc(&c->shade_radiance, (size_t)c->W * c->H) != hipSuccess) {
+      c->shade_radiance = nullptr;
+      return fail(c, FR_E_NOMEM, "fr_set_shard_plan: device allocation failed, previous plan kept");
+    }
     if (hipMalloc((void**)&new_map, nt * sizeof(uint32_t)) != hipSuccess)
       return fail(c, FR_E_NOMEM, "fr_set_shard_plan: device allocation failed, previous plan kept");
     if (hipMemcpy(new_map, map.data(), nt * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
@@ -1298,7 +1304,7 @@ int fr_shard_pack_active(fr_ctx* c, void* slab, size_t slab_bytes, uint32_t capa
   if (*count > capacity) return fail(c, FR_E_INVALID, "fr_shard_pack_active: capacity below the active pixel count");
   f4* vals = (f4*)slab;
   uint32_t* idx = (uint32_t*)((char*)slab + (size_t)capacity * sizeof(f4));
-  launch_shard_pack_active(c->active, c->ray_count, capacity, c->img[c->hist_cache], vals, idx, c->stream);
+  launch_shard_pack_active(c->active, c->ray_count, capacity, c->shade_radiance, vals, idx, c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1313,8 +1319,8 @@ int fr_shard_unpack_active(fr_ctx* c, const void* slab, size_t slab_bytes, uint3
   hipSetDevice(c->cfg.device);
   const f4* vals = (const f4*)slab;
   const uint32_t* idx = (const uint32_t*)((const char*)slab + (size_t)capacity * sizeof(f4));
-  launch_shard_unpack_active(vals, idx, count, (uint32_t)((size_t)c->W * c->H), c->img[c->hist_cache], c->img[P_shd(c)],
-                             c->stream);
+  launch_shard_unpack_active(c->U, vals, idx, count, (uint32_t)((size_t)c->W * c->H), c->img[P_wgt(c)],
+                             c->img[c->hist_cur], c->img[c->hist_cache], c->img[P_shd(c)], c->stream);
   int rc = check_launch(c);
   if (rc) return rc;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1648,6 +1654,7 @@ int check_launch(fr_ctx* c) { return ::check_launch(c); }
 void join_recon(fr_ctx* c) { ::join_recon(c); }
 int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) { return ::frame_half(c, t, trace, recon); }
 int P_shd(const fr_ctx* c) { return ::P_shd(c); }
+int P_wgt(const fr_ctx* c) { return ::P_wgt(c); }
 }  // namespace fri
 
 struct fr_scene {

@@ -21,7 +21,7 @@ size_t shade_item_store_f4();
 void launch_sample_setup(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*, f4*,
                          uint32_t*, hipStream_t);
 void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
-                          const f4*, unsigned long long*, f4*, f4*, uint32_t*, uint32_t, hipStream_t);
+                          const f4*, unsigned long long*, f4*, f4*, uint32_t*, uint32_t, f4*, hipStream_t);
 size_t shade_counter_words();
 size_t shade_fx_slots(uint32_t max_active, int spp, uint32_t handoff);
 void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
@@ -38,7 +38,8 @@ void launch_logpolar(const f4*, f4*, f4*, int, int, f2, hipStream_t);
 void launch_composite(const f4*, int, int, int, f4*, hipStream_t);
 void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
 void launch_shard_pack_active(const uint32_t*, const uint32_t*, uint32_t, const f4*, f4*, uint32_t*, hipStream_t);
-void launch_shard_unpack_active(const f4*, const uint32_t*, uint32_t, uint32_t, f4*, f4*, hipStream_t);
+void launch_shard_unpack_active(const FrameUniforms&, const f4*, const uint32_t*, uint32_t, uint32_t, const f4*, const f4*, f4*,
+                                f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, f4*, f4*, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
 void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, uint32_t*, uint32_t*, f4*, int, int, bool, bool, hipStream_t);
@@ -124,6 +125,7 @@ struct fr_ctx {
   // owner_counts_p[slot]) and copy them to pinned host memory (h_counts, ev_counts[slot]): a group
   // sizes its transfers from them without a collective (every rank computes the same full mask).
   uint32_t* shard_map = nullptr;
+  f4* shade_radiance = nullptr;    // a sharded rank's traced pixels' (tone-mapped radiance, 1), active order
   std::vector<uint8_t> shard_owner;
   uint32_t* bcount = nullptr;
   uint32_t* owner_counts_p[MAX_SLOTS] = {};
@@ -241,4 +243,5 @@ void join_recon(fr_ctx* c);
 // chains in c->recon_chains)
 int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon);
 int P_shd(const fr_ctx* c);
+int P_wgt(const fr_ctx* c);
 }  // namespace fri

@@ -205,7 +205,7 @@ int exchange(fr_group* g) {
     for (int s = 0; s < g->G; s++)
       if (L.n[s] > (size_t)g->tiles_per_vrank[s] * T2) return gfail(FR_E_STATE, "group: active count above the rank's tiles");
   }
-  // pack this rank's traced pixels: history texels, then their pixel indices (n x 20 B)
+  // pack this rank's traced pixels: (radiance, 1) texels, then their pixel indices (n x 20 B)
   for (GroupRank& L : g->loc) {
     const uint32_t n = L.n[L.vrank];
     bool any_receiver = false;
@@ -221,7 +221,7 @@ int exchange(fr_group* g) {
     }
     f4* vals = (f4*)L.send[k];
     uint32_t* idx = (uint32_t*)(L.send[k] + (size_t)n * sizeof(f4));
-    fr::launch_shard_pack_active(L.c->active, L.c->ray_count, n, L.c->img[L.c->hist_cache], vals, idx, L.c->stream);
+    fr::launch_shard_pack_active(L.c->active, L.c->ray_count, n, L.c->shade_radiance, vals, idx, L.c->stream);
     if (int rc = fri::check_launch(L.c)) return gfail(rc, fr_last_error(L.c));
     hipEventRecord(L.ev_packed, L.c->stream);
     // The slot's active list and ray count are released to the front stages of frame + nslots (stream5
@@ -271,8 +271,8 @@ int exchange(fr_group* g) {
       if (!receives(g, L.vrank, s) || !L.n[s]) continue;
       const f4* vals = (const f4*)L.recv[k][s];
       const uint32_t* idx = (const uint32_t*)(L.recv[k][s] + (size_t)L.n[s] * sizeof(f4));
-      fr::launch_shard_unpack_active(vals, idx, L.n[s], npix, L.c->img[L.c->hist_cache], L.c->img[fri::P_shd(L.c)],
-                                     L.c->stream);
+      fr::launch_shard_unpack_active(L.c->U, vals, idx, L.n[s], npix, L.c->img[fri::P_wgt(L.c)], L.c->img[L.c->hist_cur],
+                                     L.c->img[L.c->hist_cache], L.c->img[fri::P_shd(L.c)], L.c->stream);
     }
     if (int rc = fri::check_launch(L.c)) return gfail(rc, fr_last_error(L.c));
     hipEventRecord(L.ev_unpacked[k], L.c->stream);
