@@ -354,6 +354,17 @@ static bool bvh_work_reserve(BvhWork*& w, int n, hipStream_t s, std::string& err
 
 bool bvh_work_prepare(BvhWork** w, int n, hipStream_t s, std::string& err) { return bvh_work_reserve(*w, n, s, err); }
 
+// The builder's small initial values in one launch (they were three pageable host-to-device copies, which
+// go through the runtime's staging path: the first rebuilds of a context took 6-15 ms instead of 0.8-2).
+// cb: the scene box accumulators (min: +bits, max: 0); qa[0]: the root item; ctr: node_ctr, max_stack, ncur,
+// nnext, levels.
+__global__ void k_build_init(uint32_t* __restrict__ cb, CollapseItem* __restrict__ qa, uint32_t* __restrict__ ctr) {
+  const int t = threadIdx.x;
+  if (t < 6) cb[t] = t < 3 ? 0xFFFFFFFFu : 0u;
+  if (t < 5) ctr[t] = t == 0 || t == 2 ? 1u : 0u;
+  if (t == 0) qa[0] = CollapseItem{0, 0, 0};
+}
+
 // Builds the four-wide BVH of n triangles (pos: 3 vertices per triangle, device) into the caller's
 // nodes / tri / prim (device, n entries each) with the workspace *work (created or grown here, kept
 // by the caller). Returns false with err set on failure. num_nodes, max_stack and depth (levels of
@@ -364,8 +375,7 @@ bool gpu_build_bvh(BvhWork** work, const f3* pos, int n, BvhNode* nodes, TriGeo*
   if (n < 3) { err = "GPU BVH builder needs at least 3 triangles"; return false; }
   if (!bvh_work_reserve(*work, n, s, err)) return false;
   BvhWork& w = **work;
-  const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
-  hipMemcpyAsync(w.cb, init, sizeof(init), hipMemcpyHostToDevice, s);
+  hipLaunchKernelGGL(k_build_init, dim3(1), dim3(64), 0, s, w.cb, w.qa, w.ctr);
   const int B = 256, G = (n + B - 1) / B;
   hipLaunchKernelGGL(k_prim_boxes, dim3(std::min(G, 2048)), dim3(B), 0, s, pos, n, w.blo, w.bhi, w.cb);
   hipLaunchKernelGGL(k_morton, dim3(G), dim3(B), 0, s, w.blo, w.bhi, n, w.cb, w.codes, w.ids);
@@ -376,11 +386,7 @@ bool gpu_build_bvh(BvhWork** work, const f3* pos, int n, BvhNode* nodes, TriGeo*
   hipLaunchKernelGGL(k_boxes_up, dim3(G), dim3(B), 0, s, n, w.ids_s, w.blo, w.bhi, w.parent, w.child, w.nlo, w.nhi,
                      w.arrivals);
   BinTree T{n, w.child, w.range, w.nlo, w.nhi, w.blo, w.bhi, w.ids_s};
-  const CollapseItem root{0, 0, 0};
-  // ctr: node_ctr, max_stack, ncur, nnext, levels
-  const uint32_t ctr_init[5] = {1u, 0u, 1u, 0u, 0u};
-  hipMemcpyAsync(w.qa, &root, sizeof(root), hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(w.ctr, ctr_init, sizeof(ctr_init), hipMemcpyHostToDevice, s);
+  // (qa[0] = the root item and ctr = {1, 0, 1, 0, 0}: k_build_init)
   const int kBatch = 8;
   int launched = 0;
   CollapseItem *qa = w.qa, *qb = w.qb;
