@@ -462,6 +462,14 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       return bail(FR_E_NOMEM);
     }
     c->tree_full_cap = c->bvh.nodes.size() <= cap;
+    // both trees' arrays written once by the device (the GPU builder writes the spare first)
+    hipMemsetAsync(c->spare_nodes, 0, cap * sizeof(BvhNode), c->stream);
+    hipMemsetAsync(c->spare_tri, 0, cap * sizeof(TriGeo), c->stream);
+    hipMemsetAsync(c->spare_prim, 0, cap * sizeof(int32_t), c->stream);
+    hipMemsetAsync(c->d_nodes, 0, std::max(cap, c->bvh.nodes.size()) * sizeof(BvhNode), c->stream);
+    hipMemsetAsync(c->d_tri, 0, cap * sizeof(TriGeo), c->stream);
+    hipMemsetAsync(c->d_prim, 0, cap * sizeof(int32_t), c->stream);
+    if (hipStreamSynchronize(c->stream) != hipSuccess) { c->err = "device memset (scene) failed"; return bail(FR_E_HIP); }
     std::string werr;
     if (nt >= 3 && !bvh_work_prepare(&c->bvh_work, nt, c->stream, werr)) { c->err = werr; return bail(FR_E_NOMEM); }
   }

@@ -348,6 +348,14 @@ static bool bvh_work_reserve(BvhWork*& w, int n, hipStream_t s, std::string& err
     w = nullptr;
     return false;
   }
+  // every scratch array written once by a kernel here: the first rebuilds of a context were 9-22 ms, the later
+  // ones 0.8-2 ms (first device writes into fresh allocations)
+  for (auto [p, bytes] : {std::pair<void*, size_t>{w->blo, n * sizeof(f4)}, {w->bhi, n * sizeof(f4)},
+                          {w->nlo, n * sizeof(f4)}, {w->nhi, n * sizeof(f4)}, {w->codes, n * 4u}, {w->codes_s, n * 4u},
+                          {w->ids, n * 4u}, {w->ids_s, n * 4u}, {w->child, n * sizeof(int2)}, {w->range, n * sizeof(int2)},
+                          {w->parent, 2 * n * 4u}, {w->arrivals, n * 4u}, {w->qa, n * sizeof(CollapseItem)},
+                          {w->qb, n * sizeof(CollapseItem)}, {w->cnt, n * 4u}, {w->off, n * 4u}, {w->tmp, w->tmp_bytes}})
+    hipMemsetAsync(p, 0, bytes, s);
   w->cap = n;
   return true;
 }

@@ -83,11 +83,16 @@ def main():
     one = pipelined(None)
     print(json.dumps({"G": 1, "scene": scene_name, "pipelined_frame_ms": round(one, 4), "fps": round(1e3 / one, 1),
                       "pixels_received_by_recon_ranks": n_all}), flush=True)
-    for G, m in ((2, 1), (4, 1), (6, 1), (6, 2), (8, 1), (8, 2), (8, 3)):
+    layouts = ((2, 1), (4, 1), (6, 1), (6, 2), (8, 1), (8, 2), (8, 3))
+    if os.environ.get("FOVRT_MODEL_LAYOUTS"):  # e.g. "4:1,8:2": only these (G, jfa_ranks)
+        layouts = tuple(tuple(int(v) for v in x.split(":")) for x in os.environ["FOVRT_MODEL_LAYOUTS"].split(","))
+    # FOVRT_RECON_COST="a,b": the plan's reconstruction costs (fr_group_config.recon_cost; default 0.5, 0.17)
+    rc = tuple(float(v) for v in os.environ["FOVRT_RECON_COST"].split(",")) if os.environ.get("FOVRT_RECON_COST") else None
+    for G, m in layouts:
         # group.cpp's layout: view rank 0 and ranks 2..m take JFA -> Sibson in turns (cost / m each),
         # view rank 1 pull-push -> A-Trous, the rest trace; tiles by water filling
         jfa = [0] + list(range(2, m + 1))
-        owner = fovrt.group_plan(W, H, G, tile=T, jfa_ranks=m)  # the plan fr_group_create deals
+        owner = fovrt.group_plan(W, H, G, tile=T, jfa_ranks=m, recon_cost=rc)  # the plan fr_group_create deals
         tiles = np.bincount(owner, minlength=G)
         w = (tiles / tiles.sum()).tolist()
         roles = {r: 1 for r in jfa}
