@@ -17,6 +17,9 @@
 // leaf triangle counts, exclusive scan, triangle relayout.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include "fr_device.h"
@@ -348,14 +351,6 @@ static bool bvh_work_reserve(BvhWork*& w, int n, hipStream_t s, std::string& err
     w = nullptr;
     return false;
   }
-  // every scratch array written once by a kernel here: the first rebuilds of a context were 9-22 ms, the later
-  // ones 0.8-2 ms (first device writes into fresh allocations)
-  for (auto [p, bytes] : {std::pair<void*, size_t>{w->blo, n * sizeof(f4)}, {w->bhi, n * sizeof(f4)},
-                          {w->nlo, n * sizeof(f4)}, {w->nhi, n * sizeof(f4)}, {w->codes, n * 4u}, {w->codes_s, n * 4u},
-                          {w->ids, n * 4u}, {w->ids_s, n * 4u}, {w->child, n * sizeof(int2)}, {w->range, n * sizeof(int2)},
-                          {w->parent, 2 * n * 4u}, {w->arrivals, n * 4u}, {w->qa, n * sizeof(CollapseItem)},
-                          {w->qb, n * sizeof(CollapseItem)}, {w->cnt, n * 4u}, {w->off, n * 4u}, {w->tmp, w->tmp_bytes}})
-    hipMemsetAsync(p, 0, bytes, s);
   w->cap = n;
   return true;
 }
@@ -381,18 +376,32 @@ __global__ void k_build_init(uint32_t* __restrict__ cb, CollapseItem* __restrict
 bool gpu_build_bvh(BvhWork** work, const f3* pos, int n, BvhNode* nodes, TriGeo* tri, int32_t* prim, int* num_nodes,
                    int* max_stack, int* depth, hipStream_t s, std::string& err) {
   if (n < 3) { err = "GPU BVH builder needs at least 3 triangles"; return false; }
+  // FOVRT_BVH_PHASES=1: host time of each phase (each followed by a stream sync) on stderr, a diagnostic
+  static const bool phases = [] { const char* v = getenv("FOVRT_BVH_PHASES"); return v && atoi(v) != 0; }();
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char* name) {
+    if (!phases) return;
+    hipStreamSynchronize(s);
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "bvh phase %-10s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
+  phase("entry");
   if (!bvh_work_reserve(*work, n, s, err)) return false;
   BvhWork& w = **work;
   hipLaunchKernelGGL(k_build_init, dim3(1), dim3(64), 0, s, w.cb, w.qa, w.ctr);
   const int B = 256, G = (n + B - 1) / B;
   hipLaunchKernelGGL(k_prim_boxes, dim3(std::min(G, 2048)), dim3(B), 0, s, pos, n, w.blo, w.bhi, w.cb);
   hipLaunchKernelGGL(k_morton, dim3(G), dim3(B), 0, s, w.blo, w.bhi, n, w.cb, w.codes, w.ids);
+  phase("morton");
   size_t tb = w.tmp_bytes;
   hipcub::DeviceRadixSort::SortPairs(w.tmp, tb, w.codes, w.codes_s, w.ids, w.ids_s, n, 0, 30, s);
+  phase("sort");
   hipLaunchKernelGGL(k_karras, dim3(G), dim3(B), 0, s, w.codes_s, n, w.child, w.parent, w.range);
   hipMemsetAsync(w.arrivals, 0, (size_t)n * sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_boxes_up, dim3(G), dim3(B), 0, s, n, w.ids_s, w.blo, w.bhi, w.parent, w.child, w.nlo, w.nhi,
                      w.arrivals);
+  phase("karras");
   BinTree T{n, w.child, w.range, w.nlo, w.nhi, w.blo, w.bhi, w.ids_s};
   // (qa[0] = the root item and ctr = {1, 0, 1, 0, 0}: k_build_init)
   const int kBatch = 8;
@@ -413,6 +422,7 @@ bool gpu_build_bvh(BvhWork** work, const f3* pos, int n, BvhNode* nodes, TriGeo*
     if (w.host[2] == 0) break;
     if (launched >= 64) { err = "GPU BVH builder: collapse did not terminate"; return false; }
   }
+  phase("collapse");
   *num_nodes = (int)w.host[0];
   *max_stack = (int)w.host[1];
   *depth = (int)w.host[4] - 1;
@@ -420,11 +430,13 @@ bool gpu_build_bvh(BvhWork** work, const f3* pos, int n, BvhNode* nodes, TriGeo*
   hipLaunchKernelGGL(k_leaf_counts, dim3(GN), dim3(B), 0, s, nodes, nn, w.cnt);
   tb = w.tmp_bytes;
   hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.cnt, w.off, nn, s);
+  phase("scan");
   hipLaunchKernelGGL(k_emit_leaves, dim3(GN), dim3(B), 0, s, nodes, nn, w.off, w.ids_s, pos, tri, prim);
   if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) {
     err = "GPU BVH builder: kernel failure";
     return false;
   }
+  phase("emit");
   return true;
 }
 
