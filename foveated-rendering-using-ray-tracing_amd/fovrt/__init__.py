@@ -596,7 +596,8 @@ class PathTracer:
         return n.value
 
     def shard_unpack_active(self, device_ptr, capacity, count, slab_bytes=None):
-        """Scatters another rank's packed pixels into HISTORY_CACHE and SHADING."""
+        """Adds this rank's reprojected history to another rank's packed pixels (their radiance) and scatters
+        the sums into HISTORY_CACHE and SHADING."""
         nb = int(capacity) * 20 if slab_bytes is None else int(slab_bytes)
         self._check(_lib.fr_shard_unpack_active(self._ctx, C.c_void_p(device_ptr), nb, int(capacity), int(count)))
 

@@ -272,11 +272,13 @@ int fr_set_front_local(fr_ctx* ctx, int on);
  * rank can share (JFA's reach, the global pull-push pyramid). fr_set_shard = first_tracer 0. */
 int fr_set_shard_ex(fr_ctx* ctx, int rank, int count, int tile, int first_tracer);
 /* Sparse SHADING gather (SURVEY §8(e) "sparse variant"): a tracing rank packs only the pixels its last
- * trace half shaded, as capacity x 16 B of history texels followed by capacity x 4 B of pixel indices
- * (slab_bytes >= 20 x capacity, else FR_E_INVALID); *count returns their number (FR_E_INVALID when it
- * exceeds capacity: size capacity from fr_ray_count). A receiving rank, after its own trace half (which
- * carries every other pixel's history), scatters each rank's entries into HISTORY_CACHE and SHADING
- * (indices outside the screen are skipped). ~10x less than the tile slabs at a 10 % mask. Exact for a
+ * trace half shaded, as capacity x 16 B of (tone-mapped radiance, 1) texels followed by capacity x 4 B of
+ * pixel indices (slab_bytes >= 20 x capacity, else FR_E_INVALID); *count returns their number
+ * (FR_E_INVALID when it exceeds capacity: size capacity from fr_ray_count). A receiving rank, after its own
+ * trace half (which carries every other pixel's history), adds each entry's reprojected history from its
+ * own history, as the shading resolve does, and scatters the sums into HISTORY_CACHE and SHADING (indices
+ * outside the screen are skipped; the sender's own history is not used: a tile-edge pixel's reprojection
+ * can round into another rank's tiles). ~10x less than the tile slabs at a 10 % mask. Exact for a
  * static camera when the compositing rank receives; with a moving camera when every rank receives
  * every other rank's pixels each frame (its reprojection then reads a complete history). Both
  * synchronise the context stream. */
@@ -297,7 +299,7 @@ int fr_shard_unpack(fr_ctx* ctx, int buffer_id, int src_rank, const void* device
  * G = R / V ranks: rank r renders view r / G as view rank r % G (view v's camera is set on its ranks'
  * contexts with fr_set_camera as usual). In a view the screen tiles are dealt over the ranks by weight
  * (fr_shard_plan). Every rank runs the front stages (G-buffer, sampling mask, compaction) and traces its
- * own tiles' active pixels; each traced pixel (20 B: history texel + pixel index) goes to the view's
+ * own tiles' active pixels; each traced pixel (20 B: radiance texel + pixel index) goes to the view's
  * reconstruction ranks, which run JumpFlooding -> Sibson (view rank 0) and pull-push -> A-Trous (view
  * rank 1 with split_recon, else rank 0 as well); the composite is bit-identical to the one-GPU frame.
  * That gather is the path's only exchange (JFA's reach and the pull-push pyramid are global); it uses
