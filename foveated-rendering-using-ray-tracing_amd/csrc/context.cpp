@@ -464,18 +464,6 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     c->tree_full_cap = c->bvh.nodes.size() <= cap;
     std::string werr;
     if (nt >= 3 && !bvh_work_prepare(&c->bvh_work, nt, c->stream, werr)) { c->err = werr; return bail(FR_E_NOMEM); }
-    // Two builds into the spare tree (not swapped in: the scene keeps its tree). The first two builds of a
-    // context take 5-25 ms in the builder's first kernels (k_prim_boxes / k_morton, FOVRT_BVH_PHASES=1;
-    // per context, not per process; pre-touching the arrays did not help), every later one 0.8-2 ms: paid
-    // here, not in a frame loop's fr_rebuild_bvh / fr_set_positions.
-    for (int k = 0; k < 2 && nt >= 3; k++) {
-      int wn = 0, ws = 0, wd = 0;
-      if (!gpu_build_bvh(&c->bvh_work, c->d_pos, nt, c->spare_nodes, c->spare_tri, c->spare_prim, &wn, &ws, &wd,
-                         c->stream, werr)) {
-        c->err = werr;
-        return bail(FR_E_HIP);
-      }
-    }
   }
   if (cfg.bvh_builder == 0) {
     if (hipMemcpy(c->d_nodes, c->bvh.nodes.data(), c->bvh.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice) != hipSuccess ||
