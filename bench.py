@@ -528,7 +528,8 @@ def main():
                      "max_rebuild_ms": round(float(max(builds)), 3),
                      "rebuild_ms": [round(b, 3) for b in builds],
                      "note": "fr_rebuild_bvh wall time of six rebuilds in a row (median, max and all); the context "
-                             "allocated and warmed the builder at fr_create",
+                             "allocates the builder and both trees at fr_create (no allocation in a rebuild); the "
+                             "first two rebuilds after the first frames run slow (DESIGN.md section 8, row 2)",
                      "triangles": int(tracer.scene_arrays()["pos"].shape[0])}
     if rank == 0 and R == 1 and not args.no_cpu_baseline:
         try:
