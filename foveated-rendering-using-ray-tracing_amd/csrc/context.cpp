@@ -503,7 +503,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   d.envmap = s.envmap;
   d.light_position = s.light_position; d.light_v1 = s.light_v1; d.light_v2 = s.light_v2;
   d.light_normal = s.light_normal; d.light_emission = s.light_emission;
-  d.light_area = length(cross(s.light_v1, s.light_v2));
+  d.light_area = lengthc(cross(s.light_v1, s.light_v2));  // as diffuse.ptx:725-736 computes A (contracted length)
   d.bbox_min = s.bbox_min; d.bbox_max = s.bbox_max;
   d.scene_epsilon = 1.e-3f;
 

@@ -53,12 +53,34 @@ def lib():
         L.or_pullpush.argtypes = [C.c_int, C.c_int, F, F, F, F]
         L.or_atrous.argtypes = [C.c_int, C.c_int, C.c_int, F, F, F, F]
         L.or_logpolar.argtypes = [C.c_int, C.c_int, C.c_float, C.c_float, F, F, F]
+        L.or_ptx_site.restype = C.c_int
+        L.or_ptx_site.argtypes = [C.c_int, C.c_int, F, F]
         _lib = L
     return _lib
 
 
 def fp(a):
     return a.ctypes.data_as(F)
+
+
+# or_ptx_site: site ids -> (input row width, output row width); the row layouts are oracle.cpp's
+PTX_SITES = {"intersect": (0, 17, 7), "attributes": (1, 20, 8), "refine": (2, 13, 6), "camera0": (3, 23, 3),
+             "camera3": (4, 26, 3), "faceforward": (5, 6, 1), "reproject": (6, 21, 2), "gbuffer_light": (7, 18, 6),
+             "is_valid": (8, 7, 1), "gaze_dist": (9, 6, 1), "atanf": (10, 1, 1), "atan2f": (11, 2, 1),
+             "acosf": (12, 1, 1), "sinf": (13, 1, 1), "cosf": (14, 1, 1), "hemisphere": (15, 2, 3), "onb": (16, 6, 3),
+             "diffuse_light": (17, 20, 6), "refract": (18, 7, 5), "reflect": (19, 6, 3), "fresnel": (20, 3, 1),
+             "luminance": (21, 3, 1), "tonemap_rational": (22, 1, 1), "envmap_uv": (23, 3, 2), "saliency": (24, 7, 1),
+             "velocity_arg": (25, 4, 1), "velocity_sal": (26, 1, 1), "depth_sal": (27, 9, 2), "normal_enc": (28, 1, 1)}
+
+
+def ptx_site(name, rows):
+    """The oracle's own function at one PTX site (or_ptx_site) on the rows of `rows` (n x in-width)."""
+    sid, ni, no = PTX_SITES[name]
+    a = _c(rows, np.float32).reshape(-1, ni)
+    out = np.zeros((a.shape[0], no), np.float32)
+    rc = lib().or_ptx_site(sid, a.shape[0], fp(a), fp(out))
+    assert rc == no, (name, rc)
+    return out
 
 
 def _c(a, dt):
