@@ -385,6 +385,32 @@ def main():
     elapsed, total_segs = reduce_over_ranks(dist, dev, elapsed, segs)
     _, total_redundant = reduce_over_ranks(dist, dev, 0.0, redundant)
 
+    # The latency-bounded mode (fr_set_pipeline_mode LATENCY: one trace half in flight, the previous frame's
+    # reconstruction beside the next trace half) on the same workload: K more frames after a few warm-ups,
+    # wall-clock fps and the frame clock. Measured after `value`'s timed region, never inside it.
+    latency_mode = None
+    if group is None:
+        tracer.set_pipeline_mode(fovrt.PIPELINE_LATENCY)
+        for _ in range(3):
+            step(False)
+        tracer.synchronize()
+        tracer.frame_clock(True)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step(False)
+        tracer.synchronize()
+        el = time.perf_counter() - t1
+        lat, itv = tracer.frame_clock_read()
+        tracer.frame_clock(False)
+        tracer.set_pipeline_mode(fovrt.PIPELINE_THROUGHPUT)
+        latency_mode = {"fps": round(args.steps / el, 2), "ms_per_step": round(el / args.steps * 1e3, 4),
+                        "frame_clock": {"latency_ms": pct(lat), "interval_ms": pct(itv)} if len(lat) and len(itv) else None,
+                        "note": "fr_set_pipeline_mode(FR_PIPELINE_LATENCY): fr_frame waits on the host for the previous "
+                                "frame's path trace, so the gaze set before the call is sampled when the GPU can start "
+                                "the frame; the previous frame's reconstruction overlaps this trace half. Same frames "
+                                "(bit-identical results), measured after the throughput run"}
+
+
     # Per-stage HIP-event breakdown of the same frames, serialised (each frame synchronised, so the
     # stage times do not overlap the next frame): the stage table and the roofline kernel time.
     # The same frames are SURVEY §8(d)'s reconstructed-frame time: HIP events around one whole
@@ -488,6 +514,7 @@ def main():
                                 f"chains on their own streams), {n_timed} frames after 5 warm-ups, rank 0"
                                 + ("" if group is None else "; a group frame includes the exchange"),
         "frame_clock_pipelined": clock,
+        "pipeline_latency_mode": latency_mode,
         "frame_clock_note": "every frame of the timed region: latency = from where its G-buffer may start (the "
                             "gaze sample) to the end of its Sibson and A-Trous; interval = between consecutive "
                             "frames' ends (what a display sees). HIP events, one context",

@@ -475,6 +475,14 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   } else if (int rc = gpu_rebuild(c)) {
     return bail(rc);
   }
+  // (diagnostic) FOVRT_BVH_WARMUP=k: k throw-away GPU builds into the spare arrays
+  if (const char* v = getenv("FOVRT_BVH_WARMUP"); v && nt >= 3) {
+    for (int k = atoi(v); k > 0; k--) {
+      int nn = 0, ms = 0, dp = 0;
+      std::string werr;
+      gpu_build_bvh(&c->bvh_work, c->d_pos, nt, c->spare_nodes, c->spare_tri, c->spare_prim, &nn, &ms, &dp, c->stream, werr);
+    }
+  }
   DevScene& d = c->dsc;
   memset(&d, 0, sizeof(d));
   d.nodes = c->d_nodes; d.tri_geo = c->d_tri; d.tri_prim = c->d_prim; d.shade = c->d_shade;
@@ -975,6 +983,13 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     // untimed frames pipeline: the front stages go to stream5 and overlap the previous frame's
     // entry 3 (timed frames keep every stage on `stream`, one after the other)
     hipStream_t fs = t ? c->stream : c->stream5;
+    if (!t && c->pipeline_mode == FR_PIPELINE_LATENCY && c->trace_pending[c->slot]) {
+      // one trace half in flight: the previous frame's path trace (its slot's ev_trace, recorded after its
+      // resolve) ends before this frame is enqueued, so the gaze set before this call is current when the
+      // G-buffer starts; the previous frame's reconstruction keeps running beside this trace half
+      hipError_t e = hipEventSynchronize(c->ev_trace[c->slot]);
+      if (e != hipSuccess) return fail(c, FR_E_HIP, std::string("frame failed: ") + hipGetErrorString(e));
+    }
     if (!t && c->stream_dirty) {
       // the front stages overwrite buffers (gclass, DIFFUSE, EXTRA, depth, ballots, counts, lp_cache) that
       // work enqueued on `stream` by other calls may still read: order them after it explicitly
@@ -1056,6 +1071,13 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
 }
 
 int fr_frame(fr_ctx* c, fr_frame_timing* t) { return frame_half(c, t, true, true); }
+int fr_set_pipeline_mode(fr_ctx* c, int mode) {
+  if (!c) return FR_E_INVALID;
+  if (mode != FR_PIPELINE_THROUGHPUT && mode != FR_PIPELINE_LATENCY)
+    return fail(c, FR_E_INVALID, "fr_set_pipeline_mode: FR_PIPELINE_THROUGHPUT (0) or FR_PIPELINE_LATENCY (1)");
+  c->pipeline_mode = mode;
+  return FR_OK;
+}
 int fr_set_sample_sum(fr_ctx* c, int mode) {
   if (!c) return FR_E_INVALID;
   if (mode < 0 || mode > 2) return fail(c, FR_E_INVALID, "fr_set_sample_sum: mode 0 (fp32), 1 (by frame size) or 2 (fixed point)");
@@ -1090,6 +1112,10 @@ int fr_shard_unpack_active_enqueue(fr_ctx* c, const void* slab, size_t slab_byte
   const uint32_t* idx = (const uint32_t*)((const char*)slab + (size_t)capacity * sizeof(f4));
   launch_shard_unpack_active(c->U, vals, idx, count, (uint32_t)((size_t)c->W * c->H), c->img[P_wgt(c)],
                              c->img[c->hist_cur], c->img[c->hist_cache], c->img[P_shd(c)], c->stream);
+  // the unpack reads the slot's WEIGHT: the front stages of frame + nslots (stream5 waits for ev_trace[slot])
+  // may overwrite it only after this launch
+  hipEventRecord(c->ev_trace[c->slot], c->stream);
+  c->trace_pending[c->slot] = true;
   return check_launch(c);
 }
 

@@ -138,6 +138,7 @@ struct fr_ctx {
   uint8_t* front_need = nullptr;
   std::vector<uint8_t> front_need_h;
   uint32_t front_need_px = 0;
+  int pipeline_mode = 0;            // FR_PIPELINE_THROUGHPUT / FR_PIPELINE_LATENCY (fr_set_pipeline_mode)
   int recon_chains = 3;             // reconstruction chains this context runs: 1 JFA -> Sibson, 2 pull-push -> A-Trous
   hipEvent_t recon_gate = nullptr;  // when set, chain 2 (pull-push -> A-Trous) waits for it (a group's
                                     // composite reads the last A-Trous image)

@@ -277,6 +277,10 @@ int exchange(fr_group* g) {
     if (int rc = fri::check_launch(L.c)) return gfail(rc, fr_last_error(L.c));
     hipEventRecord(L.ev_unpacked[k], L.c->stream);
     L.unpacked_pending[k] = true;
+    // the unpack reads the slot's WEIGHT (the history gather): the slot goes back to the front stages of
+    // frame + nslots (stream5 waits for ev_trace[slot]) only after it, as after the pack above
+    hipEventRecord(L.c->ev_trace[L.c->slot], L.c->stream);
+    L.c->trace_pending[L.c->slot] = true;
   }
   return FR_OK;
 }

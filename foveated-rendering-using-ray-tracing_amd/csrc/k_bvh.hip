@@ -20,6 +20,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 #include "fr_device.h"
@@ -378,13 +379,23 @@ bool gpu_build_bvh(BvhWork** work, const f3* pos, int n, BvhNode* nodes, TriGeo*
   if (n < 3) { err = "GPU BVH builder needs at least 3 triangles"; return false; }
   // FOVRT_BVH_PHASES=1: host time of each phase (each followed by a stream sync) on stderr, a diagnostic
   static const bool phases = [] { const char* v = getenv("FOVRT_BVH_PHASES"); return v && atoi(v) != 0; }();
+  // (host time, and the GPU time between events recorded at the phase boundaries)
   auto t_last = std::chrono::steady_clock::now();
+  hipEvent_t ev_last = nullptr;
   auto phase = [&](const char* name) {
     if (!phases) return;
+    hipEvent_t ev = nullptr;
+    hipEventCreate(&ev);
+    hipEventRecord(ev, s);
     hipStreamSynchronize(s);
     const auto t = std::chrono::steady_clock::now();
-    fprintf(stderr, "bvh phase %-10s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(t - t_last).count());
+    float gms = 0.0f;
+    if (ev_last) { hipEventElapsedTime(&gms, ev_last, ev); hipEventDestroy(ev_last); }
+    fprintf(stderr, "bvh phase %-10s %8.3f ms host %8.3f ms gpu\n", name,
+            std::chrono::duration<double, std::milli>(t - t_last).count(), gms);
     t_last = t;
+    ev_last = ev;
+    if (!strcmp(name, "emit")) { hipEventDestroy(ev_last); ev_last = nullptr; }
   };
   phase("entry");
   if (!bvh_work_reserve(*work, n, s, err)) return false;

@@ -31,6 +31,8 @@ FR_OK, FR_E_INVALID, FR_E_HIP, FR_E_NOMEM, FR_E_IO, FR_E_STATE, FR_E_UNSUPPORTED
 # scenes / masks
 SCENE_BOX, SCENE_BUNNY, SCENE_VOKSELIA = 0, 1, 2
 MASK_SALIENCY, MASK_LOGPOLAR, MASK_UNIFORM2X2, MASK_ALL, MASK_LOGPOLAR_SIGNED = 0, 1, 2, 3, 4
+# fr_set_pipeline_mode
+PIPELINE_THROUGHPUT, PIPELINE_LATENCY = 0, 1
 SCENES = {"box": SCENE_BOX, "bunny": SCENE_BUNNY, "vokselia": SCENE_VOKSELIA}
 MASKS = {"saliency": MASK_SALIENCY, "logpolar": MASK_LOGPOLAR, "uniform": MASK_UNIFORM2X2, "all": MASK_ALL,
          "logpolar10": MASK_LOGPOLAR_SIGNED}
@@ -141,6 +143,7 @@ _SIGS = {
     "fr_composite_views": [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_frame": [C.c_void_p, C.POINTER(fr_frame_timing)],
     "fr_set_recon_chains": [C.c_void_p, C.c_int],
+    "fr_set_pipeline_mode": [C.c_void_p, C.c_int],
     "fr_set_sample_sum": [C.c_void_p, C.c_int],
     "fr_set_front_local": [C.c_void_p, C.c_int],
     "fr_shard_unpack_active_enqueue": [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32],
@@ -502,6 +505,11 @@ class PathTracer:
     def frame(self, timing=True):
         """One iteration of the FR/main.cpp:253-358 loop body on the device."""
         return self._frame(_lib.fr_frame, timing)
+
+    def set_pipeline_mode(self, mode):
+        """fr_set_pipeline_mode: PIPELINE_THROUGHPUT (0, frames enqueued back to back) or PIPELINE_LATENCY (1,
+        one trace half in flight: fr_frame waits for the previous frame's path trace before it starts)."""
+        self._check(_lib.fr_set_pipeline_mode(self._ctx, int(mode)))
 
     def set_sample_sum(self, mode):
         """fr_set_sample_sum: 0 fp32, 1 by frame size (default), 2 fixed point with the tail handoff."""

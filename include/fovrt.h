@@ -226,6 +226,19 @@ int fr_reset_gaze(fr_ctx* ctx);
  * reconstruction, so results are those of the sequential loop. With timing != NULL the frame is
  * synchronised and per-stage HIP-event times are returned. */
 int fr_frame(fr_ctx* ctx, fr_frame_timing* timing);
+/* How untimed fr_frame calls overlap (the reference's loop is serial, FR/main.cpp:253-373, so its
+ * gaze-to-image latency is its frame time):
+ *   FR_PIPELINE_THROUGHPUT (default): the host enqueues frames back to back; frame N+1's front stages
+ *     (entries 0-2) run beside frame N's path trace and frame N's reconstruction beside frame N+1's trace
+ *     half, up to the context's frame slots in flight (highest frames per second, latency ~2-3 frames);
+ *   FR_PIPELINE_LATENCY: one trace half in flight: fr_frame first waits (on the host) for the previous
+ *     frame's path trace to finish, so the gaze the caller set just before the call is sampled when the
+ *     GPU can start the frame; the previous frame's reconstruction still overlaps this frame's trace half
+ *     (latency ~ one serial frame, throughput above the serial loop's).
+ * Results are identical in both modes. */
+#define FR_PIPELINE_THROUGHPUT 0
+#define FR_PIPELINE_LATENCY 1
+int fr_set_pipeline_mode(fr_ctx* ctx, int mode);
 /* Which reconstruction chains fr_frame / fr_reconstruct_frame run on this context: bit 0 JumpFlooding ->
  * Sibson, bit 1 pull-push -> A-Trous (default 3, both; a group's split reconstruction sets 1 and 2 on
  * the two reconstruction ranks of a view). */

@@ -185,6 +185,8 @@ class PathTracer {
   // live per-launch HIP-event timing of the shading stage (off by default)
   void kernel_timing(bool on) { check(fr_kernel_timing(ctx(), on ? 1 : 0), ctx_, "kernel_timing"); }
   fr_stage_times kernel_times() { fr_stage_times t{}; check(fr_kernel_times(ctx(), &t), ctx_, "kernel_times"); return t; }
+  // FR_PIPELINE_THROUGHPUT (frames back to back) or FR_PIPELINE_LATENCY (one trace half in flight)
+  void set_pipeline_mode(int mode) { check(fr_set_pipeline_mode(ctx(), mode), ctx_, "set_pipeline_mode"); }
   // per-frame latency and display interval of pipelined frames (fr_frame_clock), in ms
   void frame_clock(bool on) { check(fr_frame_clock(ctx(), on ? 1 : 0), ctx_, "frame_clock"); }
   void frame_clock_read(std::vector<float>& latency_ms, std::vector<float>& interval_ms, int cap = 65536) {

@@ -364,6 +364,59 @@ def test_sibson_run_form_wide_discs(fovrt_mod, oracle, W, H, kind):
         assert np.abs(sf[y, x, :3] - ref).max() <= SIB_RUN_RMSE, (x, y, sf[y, x, :3], ref)
 
 
+def _sibson_counts(fovrt_mod, t):
+    """fr__sibson_counts: the last Sibson pass's list lengths (strips, wide[0], wide[1])."""
+    import ctypes as C
+    cnt = (C.c_uint32 * 3)()
+    assert fovrt_mod.load_library().fr__sibson_counts(t._ctx, cnt) == 0
+    return [int(v) for v in cnt]
+
+
+@pytest.mark.parametrize("W,H,kind", [(640, 360, "logpolar180"), (512, 288, "few"), (256, 160, "corner")])
+def test_sibson_strip_kernel_whole_image(fovrt_mod, oracle, W, H, kind, monkeypatch):
+    """k_sibson_strip (the default for discs over 2 x 64 rows) on whole images against the oracle's per-tap
+    Sibson (sibsonFS.glsl:16-49), every pixel: an off-centre signed log-polar mask (bench.py --gaze-path's
+    cursor at 180 degrees, scaled to 640 x 360), a few-seed frame and two corner seeds. The pass must list
+    strips (fr__sibson_counts), and the k_sibson_wide form (FOVRT_SIB_STRIP=0) of the same JFA output must
+    agree with it within one GL_LINEAR weight step."""
+    rng = np.random.default_rng(W + 3 * H)
+    if kind == "logpolar180":
+        m = logpolar_mask_np(W, H, W / 2 - 0.25 * H, H / 2, signed=True)
+    else:
+        m = np.zeros((H, W), np.uint8)
+        if kind == "few":
+            m[rng.integers(0, H, 5), rng.integers(0, W, 5)] = 1
+        else:
+            m[1, 2] = m[H - 3, W - 1] = 1
+    img = sparse_image(W, H, m, seed=W + H)
+    ex = _box_tracer(fovrt_mod, W, H)
+    ex.write(TN.SHADING, img)
+    fovrt_mod.JumpFlooding(ex).render(TN.SHADING)
+    coord, color = ex.read(TN.JFA_COORD), ex.read(TN.JFA_COLOR)
+    outs = {}
+    for strip in ("1", "0"):
+        monkeypatch.setenv("FOVRT_SIB_STRIP", strip)
+        ru = make_tracer(fovrt_mod, W, H, scene=0, mask=3, sibson_mode=0)
+        ru.write(TN.JFA_COORD, coord)
+        ru.write(TN.JFA_COLOR, color)
+        fovrt_mod.SibsonInterpolation(ru).render()
+        outs[strip] = ru.read(TN.SIBSON)
+        counts = _sibson_counts(fovrt_mod, ru)
+        if strip == "1":
+            assert counts[0] > 0, counts  # the strip kernel ran
+        else:
+            assert counts[0] == 0 and counts[1] + counts[2] > 0, counts
+        ru.destroy()
+    rs = oracle.sibson(coord, color)
+    sf = outs["1"]
+    assert np.isfinite(sf).all() and np.array_equal(sf[..., 3], rs[..., 3])
+    assert np.abs(sf - rs).max() <= SIB_RUN_MAX, np.abs(sf - rs).max()
+    # the reference's own f32 running sums over 10^4-10^5 taps per pixel (test_sibson_run_form_wide_discs)
+    assert (rmse_per_channel(sf, rs) <= 2e-4).all(), rmse_per_channel(sf, rs)
+    assert np.array_equal(outs["0"][..., 3], sf[..., 3])
+    assert np.abs(outs["0"] - sf).max() <= SIB_RUN_MAX, np.abs(outs["0"] - sf).max()
+
+
 def _sibson_pixel_np(coord, color, x, y):
     """One pixel of sibsonFS.glsl:16-49 in numpy: the shader's f32 position sequences (h, w += 1/size)
     walked in order, the taps outside [0, 1) or the disc dropped, GL_LINEAR + REPEAT at each tap
@@ -580,6 +633,32 @@ def test_pipelined_frames_panning_equal_stage_calls(fovrt_mod, monkeypatch, slot
                 TN.NORMAL, TN.DEPTH_CACHE, TN.WEIGHT, TN.MASK):
         assert equal_nan(a.read(tid), b.read(tid)), tid
     assert a.ray_count() == b.ray_count()
+
+
+def test_latency_pipeline_mode_equals_throughput_mode(fovrt_mod):
+    """fr_set_pipeline_mode(FR_PIPELINE_LATENCY) (one trace half in flight; the host waits for the previous
+    frame's path trace) renders the same frames as the default throughput pipelining, bit for bit, with
+    the camera panning and the gaze moving every frame; the frame clock covers every frame."""
+    W, H = 320, 192
+    a = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    b = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    a.set_pipeline_mode(fovrt_mod.PIPELINE_LATENCY)
+    a.frame_clock(True)
+    cam = fovrt_mod.Camera.preset(1, W, H)
+    for f in range(7):
+        cam.setPrevState()
+        cam.lookAt(np.asarray(cam.target) + np.array([0.01, 0.005, 0.0], np.float32))
+        for t in (a, b):
+            t.update_optix_variables(cam)
+            t.set_gaze(W / 2 + 20 * np.cos(f), (H / 2 + 20 * np.sin(f)) / 1.25)
+            t.frame(timing=False)
+    lat, itv = a.frame_clock_read()
+    a.frame_clock(False)
+    assert len(lat) == 7 and len(itv) == 6 and (lat > 0).all()
+    for tid in (TN.SHADING, TN.JFA_COLOR, TN.SIBSON, TN.PULLPUSH, TN.ATROUS, TN.HISTORY_CACHE, TN.MASK):
+        assert equal_nan(a.read(tid), b.read(tid)), tid
+    with pytest.raises(fovrt_mod.FovrtError):
+        a.set_pipeline_mode(2)
 
 
 def test_kernel_timing_counts_frames_and_leaves_results_unchanged(fovrt_mod):
