@@ -303,6 +303,7 @@ static int gpu_rebuild(fr_ctx* c) {
   Bvh b;
   b.root_count = 0; b.max_stack = max_stack; b.max_depth = depth;
   b.gpu_nodes = nn;
+  b.host_nodes = 0;
   c->bvh = std::move(b);
   return FR_OK;
 }
@@ -461,6 +462,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       c->err = "device allocation (scene) failed";
       return bail(FR_E_NOMEM);
     }
+
     c->tree_full_cap = c->bvh.nodes.size() <= cap;
     std::string werr;
     if (nt >= 3 && !bvh_work_prepare(&c->bvh_work, nt, c->stream, werr)) { c->err = werr; return bail(FR_E_NOMEM); }
@@ -475,14 +477,23 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   } else if (int rc = gpu_rebuild(c)) {
     return bail(rc);
   }
-  // (diagnostic) FOVRT_BVH_WARMUP=k: k throw-away GPU builds into the spare arrays
-  if (const char* v = getenv("FOVRT_BVH_WARMUP"); v && nt >= 3) {
-    for (int k = atoi(v); k > 0; k--) {
-      int nn = 0, ms = 0, dp = 0;
-      std::string werr;
-      gpu_build_bvh(&c->bvh_work, c->d_pos, nt, c->spare_nodes, c->spare_tri, c->spare_prim, &nn, &ms, &dp, c->stream, werr);
-    }
+  // The host-built tree's arrays go now, right after their upload, not in the first rebuild. Freeing them
+  // (tens of MB, the upload's DMA source) there cost that rebuild 2-6 ms of munmap, and the next GPU
+  // submission waited another 7-20 ms before its first kernel started (rocprofv3: the GPU idle with the
+  // work queued; profiles/r05_rebuild): the first two rebuilds of every context took 9 and 21 ms
+  // (BENCH_r04 bvh.rebuild_ms) instead of 0.8. Here the cost lands in fr_create, which synchronises.
+  if (cfg.bvh_builder == 0) {
+    c->bvh.host_nodes = (int)c->bvh.nodes.size();
+    std::vector<BvhNode>().swap(c->bvh.nodes);
+    std::vector<TriGeo>().swap(c->bvh.tri_geo);
+    std::vector<int32_t>().swap(c->bvh.tri_prim);
   }
+  if (nt >= 3) {
+    // the GPU builder's code object is loaded now (HIP loads a module at its first launch: 3-5 ms)
+    std::string werr;
+    if (!bvh_builder_warm(c->bvh_work, c->stream, werr)) { c->err = werr; return bail(FR_E_HIP); }
+  }
+  if (hipDeviceSynchronize() != hipSuccess) { c->err = "device synchronisation (scene) failed"; return bail(FR_E_HIP); }
   DevScene& d = c->dsc;
   memset(&d, 0, sizeof(d));
   d.nodes = c->d_nodes; d.tri_geo = c->d_tri; d.tri_prim = c->d_prim; d.shade = c->d_shade;
@@ -978,6 +989,17 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
   hipSetDevice(c->cfg.device);
   hipEvent_t* ev = c->ev;
   int rc;
+  // fr_frame_clock: a frame that fails after enqueue_geometry reserved its ring entry gives the entry
+  // back (it would never get its end event)
+  struct FcGuard {
+    fr_ctx* c;
+    ~FcGuard() {
+      if (c->fc_cur < 0) return;
+      c->fc_next = c->fc_cur;
+      c->fc_pending--;
+      c->fc_cur = -1;
+    }
+  } fc_guard{c};
   if (t) hipEventRecord(ev[0], c->stream);
   if (trace) {
     // untimed frames pipeline: the front stages go to stream5 and overlap the previous frame's
@@ -1710,7 +1732,7 @@ static void fill_arrays(const HostScene& s, const Bvh& bvh, f3 emission, std::ve
   for (int i = 0; i < 5; i++) { o->light[3 * i] = L[i].x; o->light[3 * i + 1] = L[i].y; o->light[3 * i + 2] = L[i].z; }
   o->bbox[0] = s.bbox_min.x; o->bbox[1] = s.bbox_min.y; o->bbox[2] = s.bbox_min.z;
   o->bbox[3] = s.bbox_max.x; o->bbox[4] = s.bbox_max.y; o->bbox[5] = s.bbox_max.z;
-  o->bvh_nodes = bvh.gpu_nodes >= 0 ? bvh.gpu_nodes : (int)bvh.nodes.size();
+  o->bvh_nodes = bvh.gpu_nodes >= 0 ? bvh.gpu_nodes : bvh.host_nodes ? bvh.host_nodes : (int)bvh.nodes.size();
   o->bvh_depth = bvh.max_depth;
   o->bvh_max_stack = bvh.max_stack;
 }

@@ -50,6 +50,7 @@ struct BvhWork;
 bool gpu_build_bvh(BvhWork**, const f3*, int, BvhNode*, TriGeo*, int32_t*, int*, int*, int*, hipStream_t, std::string&);
 void bvh_work_free(BvhWork*);
 bool bvh_work_prepare(BvhWork**, int, hipStream_t, std::string&);
+bool bvh_builder_warm(BvhWork*, hipStream_t, std::string&);
 #ifdef FR_STAMPS
 void launch_trace_queries(const DevScene&, const f4*, uint32_t, f4*, uint32_t*, hipStream_t, int);
 void diag_record_queries(f4*, uint32_t, hipStream_t);

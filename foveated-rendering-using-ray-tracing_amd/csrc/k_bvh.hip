@@ -358,6 +358,16 @@ static bool bvh_work_reserve(BvhWork*& w, int n, hipStream_t s, std::string& err
 
 bool bvh_work_prepare(BvhWork** w, int n, hipStream_t s, std::string& err) { return bvh_work_reserve(*w, n, s, err); }
 
+// One launch from this module (k_build_init on the workspace), so that its code object is loaded at
+// context creation rather than in the first rebuild.
+__global__ void k_build_init(uint32_t* __restrict__ cb, CollapseItem* __restrict__ qa, uint32_t* __restrict__ ctr);
+bool bvh_builder_warm(BvhWork* w, hipStream_t s, std::string& err) {
+  if (!w) return true;
+  hipLaunchKernelGGL(k_build_init, dim3(1), dim3(64), 0, s, w->cb, w->qa, w->ctr);
+  if (hipGetLastError() != hipSuccess) { err = "GPU BVH builder: launch failed"; return false; }
+  return true;
+}
+
 // The builder's small initial values in one launch (they were three pageable host-to-device copies, which
 // go through the runtime's staging path: the first rebuilds of a context took 6-15 ms instead of 0.8-2).
 // cb: the scene box accumulators (min: +bits, max: 0); qa[0]: the root item; ctr: node_ctr, max_stack, ncur,
@@ -384,11 +394,18 @@ bool gpu_build_bvh(BvhWork** work, const f3* pos, int n, BvhNode* nodes, TriGeo*
   hipEvent_t ev_last = nullptr;
   auto phase = [&](const char* name) {
     if (!phases) return;
+    using clk = std::chrono::steady_clock;
+    const auto a0 = clk::now();
     hipEvent_t ev = nullptr;
     hipEventCreate(&ev);
+    const auto a1 = clk::now();
     hipEventRecord(ev, s);
+    const auto a2 = clk::now();
     hipStreamSynchronize(s);
-    const auto t = std::chrono::steady_clock::now();
+    const auto t = clk::now();
+    auto ms = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    if (!strcmp(name, "entry"))
+      fprintf(stderr, "bvh entry api: create %.3f record %.3f sync %.3f ms\n", ms(a0, a1), ms(a1, a2), ms(a2, t));
     float gms = 0.0f;
     if (ev_last) { hipEventElapsedTime(&gms, ev_last, ev); hipEventDestroy(ev_last); }
     fprintf(stderr, "bvh phase %-10s %8.3f ms host %8.3f ms gpu\n", name,

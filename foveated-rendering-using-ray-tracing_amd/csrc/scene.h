@@ -41,6 +41,7 @@ struct Bvh {
   int max_depth = 0;
   int max_stack = 0;              // deepest traversal stack any root-to-leaf path can need
   int gpu_nodes = -1;             // node count of a device-built tree (its arrays stay on the device)
+  int host_nodes = 0;             // node count of a host-built tree whose arrays were released after the upload
 };
 
 enum ScenePreset { PRESET_BOX = 0, PRESET_BUNNY = 1, PRESET_VOKSELIA = 2 };

@@ -75,7 +75,11 @@ def test_gbuffer_bit_exact(fovrt_mod, oracle, scene, W, H):
 SAMPLING_CASES = ([(scene, m, 128, 96, None) for scene in (1, 2) for m in (0, 1, 2, 3, 4)]
                   + [(1, m, 100, 70, None) for m in (0, 4)]
                   + [(2, 0, 100, 70, (50.0, 0.0)), (2, 0, 128, 96, (-30.0, 500.0)), (1, 4, 100, 70, (99.5, 0.0)),
-                     (1, 0, 128, 96, (1e6, -1e6))])
+                     (1, 0, 128, 96, (1e6, -1e6))]
+                  # fractional cursors (glfw reports doubles, FR/gui.cpp:48-66): inexact gaze_dist products,
+                  # the fma.rn sites of samplingStep.ptx decide the ring and isValid pixels
+                  + [(1, 0, 128, 96, (37.3, 41.7)), (2, 4, 128, 96, (70.6, 52.35)), (2, 1, 100, 70, (33.33, 20.9)),
+                     (1, 2, 128, 96, (90.17, 13.71))])
 
 
 @pytest.mark.parametrize("mask_mode", [0, 1, 2, 3, 4])
