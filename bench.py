@@ -406,9 +406,9 @@ def main():
         latency_mode = {"fps": round(args.steps / el, 2), "ms_per_step": round(el / args.steps * 1e3, 4),
                         "frame_clock": {"latency_ms": pct(lat), "interval_ms": pct(itv)} if len(lat) and len(itv) else None,
                         "note": "fr_set_pipeline_mode(FR_PIPELINE_LATENCY): fr_frame waits on the host for the previous "
-                                "frame's path trace, so the gaze set before the call is sampled when the GPU can start "
-                                "the frame; the previous frame's reconstruction overlaps this trace half. Same frames "
-                                "(bit-identical results), measured after the throughput run"}
+                                "frame's JumpFlooding, then samples the gaze and enqueues the frame; its front stages "
+                                "overlap the previous frame's Sibson and pull-push -> A-Trous, its path trace starts "
+                                "after them. Same frames (bit-identical results), measured after the throughput run"}
 
 
     # Per-stage HIP-event breakdown of the same frames, serialised (each frame synchronised, so the
@@ -555,8 +555,8 @@ def main():
                      "max_rebuild_ms": round(float(max(builds)), 3),
                      "rebuild_ms": [round(b, 3) for b in builds],
                      "note": "fr_rebuild_bvh wall time of six rebuilds in a row (median, max and all); the context "
-                             "allocates the builder and both trees at fr_create (no allocation in a rebuild); the "
-                             "first two rebuilds after the first frames run slow (DESIGN.md section 8, row 2)",
+                             "allocates the builder and both trees at fr_create and releases the host-built tree there "
+                             "(no allocation or release in a rebuild; DESIGN.md section 8, row 2)",
                      "triangles": int(tracer.scene_arrays()["pos"].shape[0])}
     if rank == 0 and R == 1 and not args.no_cpu_baseline:
         try:

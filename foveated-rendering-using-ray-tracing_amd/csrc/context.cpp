@@ -404,6 +404,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   hipEventCreateWithFlags(&c->ev_front, hipEventDisableTiming);
   for (auto& e : c->ev_trace) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->ev_recon) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& e : c->ev_jfa) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->ev_counts) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (const char* v = getenv("FOVRT_SHADE_CHUNK_REFR")) c->chunk_refr = (uint32_t)std::max(0, atoi(v));
   if (const char* v = getenv("FOVRT_SHADE_XCD_BANDS")) c->xcd_bands = atoi(v) != 0;
@@ -631,6 +632,7 @@ int fr_destroy(fr_ctx* c) {
   if (c->ev_front) hipEventDestroy(c->ev_front);
   for (auto e : c->ev_trace) if (e) hipEventDestroy(e);
   for (auto e : c->ev_recon) if (e) hipEventDestroy(e);
+  for (auto e : c->ev_jfa) if (e) hipEventDestroy(e);
   for (auto& q : c->kt_ev)
     for (auto e : q) if (e) hipEventDestroy(e);
   for (auto& q : c->fc_ev)
@@ -1005,11 +1007,15 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     // untimed frames pipeline: the front stages go to stream5 and overlap the previous frame's
     // entry 3 (timed frames keep every stage on `stream`, one after the other)
     hipStream_t fs = t ? c->stream : c->stream5;
-    if (!t && c->pipeline_mode == FR_PIPELINE_LATENCY && c->trace_pending[c->slot]) {
-      // one trace half in flight: the previous frame's path trace (its slot's ev_trace, recorded after its
-      // resolve) ends before this frame is enqueued, so the gaze set before this call is current when the
-      // G-buffer starts; the previous frame's reconstruction keeps running beside this trace half
-      hipError_t e = hipEventSynchronize(c->ev_trace[c->slot]);
+    const bool latency = !t && c->pipeline_mode == FR_PIPELINE_LATENCY;
+    const int prev = c->slot;  // the previous frame's slot
+    if (latency && (c->jfa_pending[prev] || c->trace_pending[prev])) {
+      // one frame ahead at most: the host waits until the previous frame's JumpFlooding has ended (its
+      // path trace, when this context does not run that chain), then samples the gaze and enqueues this
+      // frame, whose front stages (G-buffer, sampling, compaction) overlap the previous frame's Sibson
+      // and pull-push -> A-Trous; its path trace starts after them (below)
+      hipError_t e = hipEventSynchronize(c->jfa_pending[prev] ? c->ev_jfa[prev] : c->ev_trace[prev]);
+      c->jfa_pending[prev] = false;
       if (e != hipSuccess) return fail(c, FR_E_HIP, std::string("frame failed: ") + hipGetErrorString(e));
     }
     if (!t && c->stream_dirty) {
@@ -1032,6 +1038,10 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
       hipEventRecord(c->ev_front, fs);
       c->front_pending = true;
     }
+    // latency mode: this frame's path trace starts after the previous frame's reconstruction. The
+    // megakernel fills every CU, so a reconstruction running beside it waited for it to end and then
+    // delayed this frame's own reconstruction (pipelined latency p50 10-12 ms against a 5.6 ms frame).
+    if (latency && c->recon_pending[prev]) hipStreamWaitEvent(c->stream, c->ev_recon[prev], 0);
     c->time_kernels = t != nullptr;
     rc = enqueue_shading(c);
     c->time_kernels = false;
@@ -1054,6 +1064,10 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     if (t) hipEventRecord(ev[20], c->stream3);
     if ((c->recon_chains & 1) && (rc = enqueue_jfa(c, FR_BUF_SHADING, c->stream3))) return rc;
     if (t) hipEventRecord(ev[21], c->stream3);
+    if (c->pipeline_mode == FR_PIPELINE_LATENCY && (c->recon_chains & 1)) {
+      hipEventRecord(c->ev_jfa[c->slot], c->stream3);
+      c->jfa_pending[c->slot] = true;
+    }
     if ((c->recon_chains & 1) && (rc = enqueue_sibson(c, c->stream3))) return rc;
     if (t) hipEventRecord(ev[22], c->stream3);
     if (c->recon_gate) hipStreamWaitEvent(c->stream2, c->recon_gate, 0);

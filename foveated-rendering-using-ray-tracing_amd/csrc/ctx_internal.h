@@ -120,6 +120,9 @@ struct fr_ctx {
   bool front_pending = false;
   bool trace_pending[MAX_SLOTS] = {};
   hipEvent_t ev_front = nullptr, ev_trace[MAX_SLOTS] = {}, ev_recon[MAX_SLOTS] = {};
+  // latency mode: the end of the slot's JumpFlooding (or of its trace half when the chain is not run here)
+  hipEvent_t ev_jfa[MAX_SLOTS] = {};
+  bool jfa_pending[MAX_SLOTS] = {};
   // Tile sharding (fr_set_shard_plan): tile -> (owner << 24 | index among the owner's tiles) on the
   // device (FrameUniforms::shard_map), and the owners on the host. With sharding on, the front stages
   // also count every rank's active pixels from the unfolded mask (bcount per 16x16 block ->

@@ -233,8 +233,9 @@ int fr_frame(fr_ctx* ctx, fr_frame_timing* timing);
  *     half, up to the context's frame slots in flight (highest frames per second, latency ~2-3 frames);
  *   FR_PIPELINE_LATENCY: one trace half in flight: fr_frame first waits (on the host) for the previous
  *     frame's path trace to finish, so the gaze the caller set just before the call is sampled when the
- *     GPU can start the frame; the previous frame's reconstruction still overlaps this frame's trace half
- *     (latency ~ one serial frame, throughput above the serial loop's).
+ *     GPU can start the frame; the previous frame's reconstruction overlaps this frame's front stages
+ *     (G-buffer, sampling, compaction) and ends before its path trace starts (latency ~ 1.2 serial
+ *     frames, throughput above the serial loop's).
  * Results are identical in both modes. */
 #define FR_PIPELINE_THROUGHPUT 0
 #define FR_PIPELINE_LATENCY 1
