@@ -38,6 +38,9 @@ void launch_logpolar(const f4*, f4*, f4*, int, int, f2, hipStream_t);
 void launch_composite(const f4*, int, int, int, f4*, hipStream_t);
 void launch_shard_unpack(const FrameUniforms&, int, const f4*, f4*, hipStream_t);
 void launch_shard_pack_active(const uint32_t*, const uint32_t*, uint32_t, const f4*, f4*, uint32_t*, hipStream_t);
+// the history validity rings of a still-camera group (k_trace.hip): FR_VRING pixels inside each tile
+void launch_vring_pack(const f4*, int, int, int, const int32_t*, int, uint32_t*, hipStream_t);
+void launch_vring_unpack(const uint32_t*, int, int, int, const int32_t*, int, f4*, hipStream_t);
 void launch_shard_unpack_active(const FrameUniforms&, const f4*, const uint32_t*, uint32_t, uint32_t, const f4*, const f4*, f4*,
                                 f4*, hipStream_t);
 void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, f4*, f4*, hipStream_t);

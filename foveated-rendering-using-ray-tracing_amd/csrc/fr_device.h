@@ -7,6 +7,7 @@
 namespace fr {
 
 #define FR_BVH_STACK 24  // per-lane traversal stack entries (LDS; one per BVH level)
+#define FR_VRING 2       // history validity ring inside each tile of a still-camera group (k_vring_pack)
 
 enum MaterialType : int32_t { MATL_DIFFUSE = 0, MATL_REFLECTION = 1, MATL_REFRACTION = 2 };
 

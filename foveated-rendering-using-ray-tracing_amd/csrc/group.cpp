@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -40,6 +41,11 @@ struct GroupRank {
   hipEvent_t ev_packed = nullptr, ev_comm[2] = {}, ev_unpacked[2] = {}, ev_out = nullptr, ev_sent_out = nullptr;
   bool comm_pending[2] = {}, unpacked_pending[2] = {};
   uint32_t n[FR_GROUP_MAX_VIEW_RANKS] = {};  // this frame's active pixels of every view rank
+  // history validity rings (still camera, k_vring_pack): the tile list grouped by owner (device), this
+  // rank's packed ring bits and one receive slab per other view rank, double-buffered by frame parity
+  int32_t* tiles_dev = nullptr;
+  uint32_t* vsend[2] = {};
+  std::vector<uint32_t*> vrecv[2];
   // composite (rank 0): the views' A-Trous images and the side-by-side result
   f4* comp_stack = nullptr;
   f4* comp_out = nullptr;
@@ -55,6 +61,7 @@ struct fr_group {
   fr_group_config cfg;
   std::vector<uint8_t> owner;       // tile -> view rank (the same plan in every view)
   std::vector<int> tiles_per_vrank;
+  std::vector<int> tile_off;        // view rank s's tiles: tiles_dev[tile_off[s] .. tile_off[s + 1])
   int jfa_ranks = 1;                // view ranks taking JFA -> Sibson in turns (fr_group_config.jfa_ranks)
   uint64_t frame = 0;
   bool composite_done = false;
@@ -89,6 +96,21 @@ bool receives(const fr_group* g, int r, int s) {
   if (r == s) return false;
   return g->cfg.moving_camera ? true : chains_of(g, r) != 0;
 }
+
+// Does view rank r take the other ranks' history validity rings? A pure tracer of a still camera: it holds
+// the history of its own tiles only, and its seeds read the validity of the pixels around them.
+bool vring_receiver(const fr_group* g, int r) {
+  // (FOVRT_GROUP_VRING=0: no rings, a diagnostic that shows what they fix)
+  static const bool on = [] { const char* v = getenv("FOVRT_GROUP_VRING"); return !v || atoi(v) != 0; }();
+  return on && g->G > 1 && !g->cfg.moving_camera && chains_of(g, r) == 0 && g->tiles_per_vrank[r] > 0;
+}
+bool vring_sender(const fr_group* g, int s) {
+  if (g->G == 1 || g->cfg.moving_camera || !g->tiles_per_vrank[s]) return false;
+  for (int r = 0; r < g->G; r++)
+    if (r != s && vring_receiver(g, r)) return true;
+  return false;
+}
+size_t vring_words(const fr_group* g, int s) { return (size_t)g->tiles_per_vrank[s] * (FR_VRING * g->cfg.tile / 8); }
 
 // Water filling: rank r carries recon work c[r] (in units of one frame's trace work) and gets a trace share
 // s[r] = max(0, lambda - c[r]) with sum s = 1, so that every loaded rank ends at lambda.
@@ -183,12 +205,15 @@ void free_rank(GroupRank& L) {
   for (int k = 0; k < 2; k++) {
     if (L.send[k]) hipFree(L.send[k]);
     for (char* p : L.recv[k]) if (p) hipFree(p);
+    if (L.vsend[k]) hipFree(L.vsend[k]);
+    for (uint32_t* p : L.vrecv[k]) if (p) hipFree(p);
     if (L.ev_comm[k]) hipEventDestroy(L.ev_comm[k]);
     if (L.ev_unpacked[k]) hipEventDestroy(L.ev_unpacked[k]);
   }
   if (L.ev_packed) hipEventDestroy(L.ev_packed);
   if (L.ev_out) hipEventDestroy(L.ev_out);
   if (L.ev_sent_out) hipEventDestroy(L.ev_sent_out);
+  if (L.tiles_dev) hipFree(L.tiles_dev);
   if (L.comp_stack) hipFree(L.comp_stack);
   if (L.comp_out) hipFree(L.comp_out);
   if (L.comm) hipStreamDestroy(L.comm);
@@ -231,6 +256,22 @@ int exchange(fr_group* g) {
     L.c->trace_pending[L.c->slot] = true;
     if (g->comm) hipStreamWaitEvent(L.comm, L.ev_packed, 0);
   }
+  // the history validity rings of this frame's history (after the trace half: resolve and carry)
+  for (GroupRank& L : g->loc) {
+    if (!vring_sender(g, L.vrank)) continue;
+    hipSetDevice(L.c->cfg.device);
+    if (g->comm) {
+      if (L.comm_pending[k]) hipStreamWaitEvent(L.c->stream, L.ev_comm[k], 0);
+    } else {
+      for (GroupRank& D : g->loc)
+        if (D.comm_pending[k]) hipStreamWaitEvent(L.c->stream, D.ev_comm[k], 0);
+    }
+    fr::launch_vring_pack(L.c->img[L.c->hist_cache], g->W, g->H, g->cfg.tile, L.tiles_dev + g->tile_off[L.vrank],
+                          g->tiles_per_vrank[L.vrank], L.vsend[k], L.c->stream);
+    if (int rc = fri::check_launch(L.c)) return gfail(rc, fr_last_error(L.c));
+    hipEventRecord(L.ev_packed, L.c->stream);
+    if (g->comm) hipStreamWaitEvent(L.comm, L.ev_packed, 0);
+  }
   // receive slabs of frame - 2 must have been unpacked
   for (GroupRank& L : g->loc)
     if (L.unpacked_pending[k]) {
@@ -253,11 +294,38 @@ int exchange(fr_group* g) {
       }
     }
   }
+  for (GroupRank& L : g->loc) {
+    const int v = L.view;
+    for (int s = 0; s < g->G; s++) {
+      for (int r = 0; r < g->G; r++) {
+        if (r == s || !vring_receiver(g, r) || !vring_sender(g, s)) continue;
+        const int src = rank_of(g, v, s), dst = rank_of(g, v, r);
+        if (src != L.rank && dst != L.rank) continue;
+        if (!g->comm && src != L.rank) continue;
+        const GroupRank* D = g->comm ? &L : &g->loc[dst];
+        xs.push_back({src, dst, g->comm ? (src == L.rank ? L.vsend[k] : nullptr) : L.vsend[k],
+                      dst == D->rank ? D->vrecv[k][s] : nullptr, vring_words(g, s) * sizeof(uint32_t)});
+      }
+    }
+  }
   if (int rc = run_xfers(g, xs, true)) return rc;
   for (GroupRank& L : g->loc) {
     hipSetDevice(L.c->cfg.device);
     hipEventRecord(L.ev_comm[k], L.comm);
     L.comm_pending[k] = true;
+  }
+  // a pure tracer writes the other ranks' validity rings into this frame's history (its next frame's seeds)
+  for (GroupRank& L : g->loc) {
+    if (!vring_receiver(g, L.vrank)) continue;
+    hipSetDevice(L.c->cfg.device);
+    hipStreamWaitEvent(L.c->stream, L.ev_comm[k], 0);
+    for (int s = 0; s < g->G; s++)
+      if (s != L.vrank && vring_sender(g, s))
+        fr::launch_vring_unpack(L.vrecv[k][s], g->W, g->H, g->cfg.tile, L.tiles_dev + g->tile_off[s],
+                                g->tiles_per_vrank[s], L.c->img[L.c->hist_cache], L.c->stream);
+    if (int rc = fri::check_launch(L.c)) return gfail(rc, fr_last_error(L.c));
+    hipEventRecord(L.ev_unpacked[k], L.c->stream);
+    L.unpacked_pending[k] = true;
   }
   // scatter the received pixels into HISTORY_CACHE and SHADING (after this rank's own trace half)
   const uint32_t npix = (uint32_t)((size_t)g->W * g->H);
@@ -435,6 +503,14 @@ int fr_group_create(fr_ctx* const* ctxs, int n, void* rccl_comm, const fr_group_
     if (int rc = group_plan(g->W, g->H, G, cfg, g->owner.data(), ntiles)) return bail(rc);
     for (uint8_t o : g->owner) g->tiles_per_vrank[o]++;
   }
+  std::vector<int32_t> tiles_by_owner;
+  g->tile_off.assign(G + 1, 0);
+  for (int o = 0; o < G && G > 1; o++) {
+    g->tile_off[o] = (int)tiles_by_owner.size();
+    for (size_t t = 0; t < ntiles; t++)
+      if (g->owner[t] == o) tiles_by_owner.push_back((int32_t)t);
+  }
+  g->tile_off[G] = (int)tiles_by_owner.size();
   g->loc.resize(n);
   for (int i = 0; i < n; i++) {
     GroupRank& L = g->loc[i];
@@ -476,6 +552,20 @@ int fr_group_create(fr_ctx* const* ctxs, int n, void* rccl_comm, const fr_group_
         if (receives(g, L.vrank, s) && g->tiles_per_vrank[s] &&
             hipMalloc((void**)&L.recv[k][s], (size_t)g->tiles_per_vrank[s] * T2 * 20) != hipSuccess)
           return bail(gfail(FR_E_NOMEM, "group: receive slab"));
+    }
+    if (G > 1 && !cfg.moving_camera) {
+      if (hipMalloc((void**)&L.tiles_dev, tiles_by_owner.size() * sizeof(int32_t)) != hipSuccess ||
+          hipMemcpy(L.tiles_dev, tiles_by_owner.data(), tiles_by_owner.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(gfail(FR_E_NOMEM, "group: tile list"));
+      for (int k = 0; k < 2; k++) {
+        L.vrecv[k].assign(G, nullptr);
+        if (vring_sender(g, L.vrank) && hipMalloc((void**)&L.vsend[k], vring_words(g, L.vrank) * sizeof(uint32_t)) != hipSuccess)
+          return bail(gfail(FR_E_NOMEM, "group: validity ring slab"));
+        for (int s2 = 0; s2 < G; s2++)
+          if (s2 != L.vrank && vring_receiver(g, L.vrank) && vring_sender(g, s2) &&
+              hipMalloc((void**)&L.vrecv[k][s2], vring_words(g, s2) * sizeof(uint32_t)) != hipSuccess)
+            return bail(gfail(FR_E_NOMEM, "group: validity ring slab"));
+      }
     }
     if (cfg.composite && L.rank == 0) {
       const size_t img = (size_t)g->W * g->H;

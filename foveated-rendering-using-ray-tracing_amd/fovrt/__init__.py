@@ -374,6 +374,11 @@ class PathTracer:
         self.destroy()
 
     def destroy(self):
+        # a group over this context goes first (fr_group_destroy reads its contexts; under garbage
+        # collection of a cycle the tracers' finalisers can run before the group's)
+        for grp in getattr(self, "_groups", ()):
+            grp.destroy()  # (strong references: weak ones are cleared before a cycle's finalisers run)
+        self._groups = []
         if getattr(self, "_ctx", None) is not None and _lib is not None:
             _lib.fr_destroy(self._ctx)
             self._ctx = None
@@ -812,6 +817,10 @@ class Group:
         self._comm = _comm
         self._owns_comm = False
         self.config = cfg
+        for t in self.tracers:
+            if not hasattr(t, "_groups"):
+                t._groups = []
+            t._groups.append(self)
 
     @classmethod
     def rccl(cls, tracer, unique_id: bytes, nranks, rank, **kw):

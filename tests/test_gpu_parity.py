@@ -1011,7 +1011,11 @@ GROUP_CASES = [  # (ranks, views, tile, split, moving, W, H, mask, jfa_ranks)
     (3, 1, 32, False, False, 200, 136, 4, 0), (4, 2, 32, True, False, 200, 136, 4, 0), (2, 1, 32, True, True, 160, 112, 0, 0),
     (3, 1, 16, True, True, 160, 112, 4, 0), (4, 1, 128, True, False, 3840, 2160, 4, 0),
     (4, 1, 32, True, False, 200, 136, 4, 2), (6, 2, 32, True, True, 160, 112, 4, 2), (4, 1, 16, True, False, 200, 136, 0, 3),
-    (8, 1, 128, True, False, 3840, 2160, 4, 0)]
+    (8, 1, 128, True, False, 3840, 2160, 4, 0),
+    # "drift": the camera turns by under a pixel per frame while the group keeps its still-camera mode
+    # (tile-local front, no traced pixels to the tracers): reprojections round into the neighbouring
+    # tiles, whose history validity the pure tracer takes from the rings (k_vring_pack)
+    (3, 1, 32, True, "drift", 200, 136, 4, 0), (4, 1, 16, True, "drift", 200, 136, 0, 0)]
 GROUP_SCENE = (1, 4, 3)  # bunny, 4 spp, diffuse_max_depth 3 (configs[2])
 # BASELINE.json configs[3] and [4] as their own group shapes (scene, spp, diffuse_max_depth appended):
 #   C4 vokselia 4K, 8 spp, saliency mask, one view tiled over 4 ranks;
@@ -1049,7 +1053,7 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
         cam.setPosition(np.asarray(cam.pos) + np.array([0.064 * (v - (V - 1) / 2), 0, 0], np.float32))
         cam.lookAt(cam.target)
         cams.append(cam)
-    g = fovrt_mod.Group(ranks, views=V, tile=tile, split_recon=split, moving_camera=moving, composite=True,
+    g = fovrt_mod.Group(ranks, views=V, tile=tile, split_recon=split, moving_camera=moving is True, composite=True,
                         jfa_ranks=jfa)
     info = [g.rank_info(i) for i in range(R)]
     assert sum(i["tiles"] for i in info[:G]) == ((W + tile - 1) // tile) * ((H + tile - 1) // tile)
@@ -1057,7 +1061,8 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
         for v in range(V):
             if moving:
                 cams[v].setPrevState()
-                cams[v].lookAt(np.asarray(cams[v].target) + np.array([0.02, 0.01, 0.0], np.float32))
+                step = [0.02, 0.01, 0.0] if moving is True else [0.025, 0.0, 0.0]
+                cams[v].lookAt(np.asarray(cams[v].target) + np.array(step, np.float32))
             fulls[v].update_optix_variables(cams[v])
             for r in range(v * G, (v + 1) * G):
                 ranks[r].update_optix_variables(cams[v])
@@ -1069,6 +1074,7 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
     comp = out.cpu().numpy().reshape(H, V * W, 4)
     owners = g.tile_owners(W, H)
     own_px = np.repeat(np.repeat(owners, tile, 0), tile, 1)[:H, :W]
+    n_foreign_src = 0  # tracers' own pixels whose history source lies in another rank's tiles
     for v in range(V):
         full = fulls[v]
         jfa_rank, at_rank = g.output_ranks(v)
@@ -1076,7 +1082,7 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
         assert jfa_rank == v * G + (0 if 3 % m == 0 else 3 % m + 1) and at_rank == v * G + (1 if split and G > 1 else 0)
         for r in range(v * G, (v + 1) * G):
             ch = info[r]["chains"]
-            if ch or moving:
+            if ch or moving is True:
                 for tid in (TN.SHADING, TN.HISTORY_CACHE):
                     assert equal_nan(ranks[r].read(tid), full.read(tid)), (v, r, tid)
             else:  # a still camera's tracer runs a tile-local front: its own tiles equal the full frame
@@ -1086,10 +1092,25 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
                 # ... except the pixels whose history comes (reprojection rounded across a tile edge, possibly
                 # through a chain of such pixels) from another rank's tiles: the receivers add that history
                 # themselves (k_shard_unpack_active), nothing reads the tracer's value there
-                hsel = sel & ~foreign_history(full.read(TN.WEIGHT), sel)
-                assert hsel.sum() >= 0.99 * sel.sum()
-                for tid in (TN.SHADING, TN.HISTORY_CACHE):
-                    assert equal_nan(ranks[r].read(tid)[hsel], full.read(tid)[hsel]), (v, r, tid)
+                # the history validity (.w > 0, which picks a traced pixel's seed) of the ring around its
+                # tiles comes from the owners (k_vring_pack / unpack, FR_VRING = 2 pixels inside every tile)
+                yy, xx = np.mgrid[0:H, 0:W]
+                ring = ((xx % tile < 2) | (xx % tile >= tile - 2) | (yy % tile < 2) | (yy % tile >= tile - 2)) & ~sel
+                vt, vf = ranks[r].read(TN.HISTORY_CACHE)[..., 3] > 0, full.read(TN.HISTORY_CACHE)[..., 3] > 0
+                assert np.array_equal(vt[ring], vf[ring]), (v, r, int((vt[ring] != vf[ring]).sum()))
+                # ... so every own pixel sees the one-GPU validity at its (still camera: adjacent) source
+                wf = full.read(TN.WEIGHT).astype(np.float64)
+                rnd = lambda a: np.clip(np.trunc(a + np.copysign(0.5, a)), 0, 2.0 ** 32 - 1)
+                sx, sy = np.clip(rnd(wf[..., 0]), 0, W - 1).astype(int), np.clip(rnd(wf[..., 1]), 0, H - 1).astype(int)
+                src_ok = sel & (wf[..., 2] > 0)
+                assert (np.abs(sx - xx)[src_ok] <= 1).all() and (np.abs(sy - yy)[src_ok] <= 1).all()  # within the ring
+                assert np.array_equal(vt[sy, sx][src_ok], vf[sy, sx][src_ok]), (v, r)
+                n_foreign_src += int((src_ok & ~sel[sy, sx]).sum())
+                if moving is False:  # (a drifting camera's history chains cross tiles frame after frame)
+                    hsel = sel & ~foreign_history(full.read(TN.WEIGHT), sel)
+                    assert hsel.sum() >= 0.99 * sel.sum()
+                    for tid in (TN.SHADING, TN.HISTORY_CACHE):
+                        assert equal_nan(ranks[r].read(tid)[hsel], full.read(tid)[hsel]), (v, r, tid)
                 assert ranks[r].stats()["gbuffer_primary"] < full.stats()["gbuffer_primary"]
             if r == jfa_rank:
                 for tid in (TN.JFA_COLOR, TN.SIBSON):
@@ -1100,6 +1121,9 @@ def test_group_frames_equal_single_context(fovrt_mod, R, V, tile, split, moving,
         assert equal_nan(comp[:, v * W:(v + 1) * W], full.read(TN.ATROUS)), v
         chains = [info[r]["chains"] for r in range(v * G, (v + 1) * G)]
         assert chains[0] & 1 and any(c & 2 for c in chains)
+    print("tracer pixels with a foreign history source:", n_foreign_src)
+    if moving == "drift":  # reprojections round across tile edges: the case the rings exist for
+        assert n_foreign_src > 0
     g.destroy()
     for t in ranks + fulls:
         t.destroy()
