@@ -406,9 +406,11 @@ def main():
         latency_mode = {"fps": round(args.steps / el, 2), "ms_per_step": round(el / args.steps * 1e3, 4),
                         "frame_clock": {"latency_ms": pct(lat), "interval_ms": pct(itv)} if len(lat) and len(itv) else None,
                         "note": "fr_set_pipeline_mode(FR_PIPELINE_LATENCY): fr_frame waits on the host for the previous "
-                                "frame's JumpFlooding, then samples the gaze and enqueues the frame; its front stages "
+                                "frame's JumpFlooding (and, just in time, for the part of its Sibson the front stages "
+                                "would not cover), then samples the gaze and enqueues the frame; its front stages "
                                 "overlap the previous frame's Sibson and pull-push -> A-Trous, its path trace starts "
-                                "after them. Same frames (bit-identical results), measured after the throughput run"}
+                                "after them. Same frames (bit-identical results), measured after the throughput run; "
+                                "fps = frames / wall time, to compare with fps_serial_mean on a varying workload"}
 
 
     # Per-stage HIP-event breakdown of the same frames, serialised (each frame synchronised, so the
@@ -510,6 +512,7 @@ def main():
         "frames_per_s_total": round(views * K / elapsed, 2),
         "frame_ms_serial": serial,
         "fps_serial": round(1e3 / serial["p50"], 2),
+        "fps_serial_mean": round(1e3 / float(np.mean(totals)), 2),
         "frame_ms_serial_note": f"HIP events around one synchronised frame (update -> A-Trous, the two reconstruction "
                                 f"chains on their own streams), {n_timed} frames after 5 warm-ups, rank 0"
                                 + ("" if group is None else "; a group frame includes the exchange"),

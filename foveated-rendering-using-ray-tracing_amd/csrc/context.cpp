@@ -382,7 +382,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (hipSetDevice(cfg.device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(FR_E_HIP); }
   // Stream priorities (FOVRT_STREAM_PRIORITY, A/B knob): 0 (default) all streams at the default
   // priority; 1 trace half (context stream, carry, front stages) high, reconstruction low; 2 the
-  // reconstruction high, the trace half low; 3 only the front stages high.
+  // reconstruction high, the trace half low; 3 only the front stages high; 4 JumpFlooding -> Sibson high,
+  // pull-push -> A-Trous and the front stages low.
   static const int prio_mode = [] {
     const char* v = getenv("FOVRT_STREAM_PRIORITY");
     return v ? atoi(v) : 0;
@@ -391,10 +392,11 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (prio_mode) hipDeviceGetStreamPriorityRange(&lo, &hi);
   const int p_trace = prio_mode == 1 ? hi : prio_mode == 2 ? lo : 0;
   const int p_recon = prio_mode == 1 ? lo : prio_mode == 2 ? hi : 0;
-  const int p_front = prio_mode == 1 || prio_mode == 3 ? hi : prio_mode == 2 ? lo : 0;
+  const int p_front = prio_mode == 1 || prio_mode == 3 ? hi : prio_mode == 2 || prio_mode == 4 ? lo : 0;
+  const int p_jfa = prio_mode == 4 ? hi : p_recon, p_pp = prio_mode == 4 ? lo : p_recon;
   if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, p_trace) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, p_recon) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, p_recon) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, p_pp) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, p_jfa) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, p_trace) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, p_front) != hipSuccess) {
     c->err = "stream create failed";
@@ -405,6 +407,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   for (auto& e : c->ev_trace) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->ev_recon) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->ev_jfa) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& row : c->lat_ev) for (auto& e : row) hipEventCreate(&e);
   for (auto& e : c->ev_counts) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (const char* v = getenv("FOVRT_SHADE_CHUNK_REFR")) c->chunk_refr = (uint32_t)std::max(0, atoi(v));
   if (const char* v = getenv("FOVRT_SHADE_XCD_BANDS")) c->xcd_bands = atoi(v) != 0;
@@ -553,7 +556,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     return bail(FR_E_NOMEM);
   }
   memset(c->h_counts, 0, sizeof(uint32_t) * fr_ctx::MAX_SLOTS * FR_MAX_SHARD_RANKS);
-  if (dalloc(&c->gclass, N) != hipSuccess || dalloc(&c->lp_cache, N) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
+  if (dalloc(&c->gclass, N) != hipSuccess || dalloc(&c->lp_cache, N) != hipSuccess ||
+      dalloc(&c->lp_inv, logpolar_inv_words(c->W, c->H)) != hipSuccess || dalloc(&c->words, nwords) != hipSuccess ||
       dalloc(&c->counts, 4 * nblocks) != hipSuccess || dalloc(&c->offsets, 4 * nblocks) != hipSuccess ||
       dalloc(&c->tiles, 1024) != hipSuccess || dalloc(&c->jfa_a, N) != hipSuccess || dalloc(&c->jfa_b, N) != hipSuccess ||
       dalloc(&c->pull, atlas) != hipSuccess || dalloc(&c->push, atlas) != hipSuccess ||
@@ -626,13 +630,14 @@ int fr_destroy(fr_ctx* c) {
   fr(c->bcount); fr(c->shard_map); fr(c->front_need); fr(c->shade_radiance);
   if (c->h_counts) hipHostFree(c->h_counts);
   for (auto e : c->ev_counts) if (e) hipEventDestroy(e);
-  fr(c->gclass); fr(c->lp_cache); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->item_store); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
+  fr(c->gclass); fr(c->lp_cache); fr(c->lp_inv); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->item_store); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks); fr(c->sib_wide); fr(c->sib_strips); fr(c->sib_rowp);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->ev_front) hipEventDestroy(c->ev_front);
   for (auto e : c->ev_trace) if (e) hipEventDestroy(e);
   for (auto e : c->ev_recon) if (e) hipEventDestroy(e);
   for (auto e : c->ev_jfa) if (e) hipEventDestroy(e);
+  for (auto& row : c->lat_ev) for (auto e : row) if (e) hipEventDestroy(e);
   for (auto& q : c->kt_ev)
     for (auto e : q) if (e) hipEventDestroy(e);
   for (auto& q : c->fc_ev)
@@ -713,6 +718,7 @@ static int enqueue_geometry(fr_ctx* c, hipStream_t fs) {
     hipStreamWaitEvent(fs, c->ev_trace[sl], 0);
     c->trace_pending[sl] = false;
   }
+  if (c->lat_arm) hipEventRecord(c->lat_ev[sl][0], fs);
   if (c->fc_arm) {  // fr_frame_clock: where this frame's G-buffer (the first stage to read the gaze) may start
     const int i = c->fc_next;
     if (c->fc_pending == fr_ctx::FC_RING) { fc_harvest(c, i); c->fc_pending--; }
@@ -749,7 +755,7 @@ static int enqueue_sampling(fr_ctx* c, hipStream_t fs) {
   if (lp_refresh) { c->lp_mode = c->U.mask_mode; c->lp_gaze = c->U.gaze; }
   launch_sampling(c->U, c->dsc, c->img[P_pos(c)], c->img[c->depth_cur], c->img[c->depth_cache], c->img[P_wgt(c)],
                   c->img[P_nrm(c)], c->img[P_DIFFUSE], c->img[P_EXTRA], c->mask, c->gclass, c->words, c->counts,
-                  c->cfg.write_extra, c->lp_cache, lp_refresh, c->U.shard_count > 1 ? c->bcount : nullptr, fs);
+                  c->cfg.write_extra, c->lp_cache, c->lp_inv, lp_refresh, c->U.shard_count > 1 ? c->bcount : nullptr, fs);
   if (c->U.shard_count > 1) {
     // every rank's active count of this frame (fr_shard_counts, the group's transfer sizes), to pinned
     // host memory with its own event: reading it waits for this frame's front stages only
@@ -1014,9 +1020,34 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
       // path trace, when this context does not run that chain), then samples the gaze and enqueues this
       // frame, whose front stages (G-buffer, sampling, compaction) overlap the previous frame's Sibson
       // and pull-push -> A-Trous; its path trace starts after them (below)
-      hipError_t e = hipEventSynchronize(c->jfa_pending[prev] ? c->ev_jfa[prev] : c->ev_trace[prev]);
-      c->jfa_pending[prev] = false;
+      // (polled: a blocking wait woke the host up to milliseconds late, and the GPU idled meanwhile)
+      hipEvent_t w = c->jfa_pending[prev] ? c->ev_jfa[prev] : c->ev_trace[prev];
+      hipError_t e;
+      while ((e = hipEventQuery(w)) == hipErrorNotReady) {
+      }
       if (e != hipSuccess) return fail(c, FR_E_HIP, std::string("frame failed: ") + hipGetErrorString(e));
+      // Just in time: the front stages should end when the previous frame's Sibson does (its path trace
+      // waits for both). A completed frame's times estimate the two; when its Sibson took longer than its
+      // front stages, the host waits the difference more (an eye-tracked gaze's big discs: 2-5 ms of
+      // Sibson against ~1.3 ms of front stages), so the gaze is sampled that much later.
+      for (int k = 0; k < c->nslots; k++) {
+        if (!c->lat_rec[k] || hipEventQuery(c->lat_ev[k][3]) != hipSuccess) continue;
+        float f = 0.0f, sb = 0.0f;
+        if (hipEventElapsedTime(&f, c->lat_ev[k][0], c->lat_ev[k][1]) == hipSuccess &&
+            hipEventElapsedTime(&sb, c->lat_ev[k][2], c->lat_ev[k][3]) == hipSuccess) {
+          c->lat_front_ms = f;
+          c->lat_sib_ms = sb;
+        }
+        c->lat_rec[k] = false;
+      }
+      const float delay_ms = c->jfa_pending[prev] ? c->lat_sib_ms - c->lat_front_ms : 0.0f;
+      if (delay_ms > 0.05f) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count() < delay_ms &&
+               hipEventQuery(c->ev_recon[prev]) == hipErrorNotReady) {
+        }
+      }
+      c->jfa_pending[prev] = false;
     }
     if (!t && c->stream_dirty) {
       // the front stages overwrite buffers (gclass, DIFFUSE, EXTRA, depth, ballots, counts, lp_cache) that
@@ -1026,9 +1057,10 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     }
     c->stream_dirty = false;
     c->fc_arm = c->fc_on && recon;  // whole frames only (a group's trace half has no end of its own)
+    c->lat_arm = latency && recon;
     rc = enqueue_geometry(c, fs);
     c->fc_arm = false;
-    if (rc) return rc;
+    if (rc) { c->lat_arm = false; return rc; }
     if (t) hipEventRecord(ev[1], c->stream);
     if ((rc = enqueue_sampling(c, fs))) return rc;
     if (t) hipEventRecord(ev[2], c->stream);
@@ -1038,6 +1070,7 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
       hipEventRecord(c->ev_front, fs);
       c->front_pending = true;
     }
+    if (c->lat_arm) hipEventRecord(c->lat_ev[c->slot][1], fs);
     // latency mode: this frame's path trace starts after the previous frame's reconstruction. The
     // megakernel fills every CU, so a reconstruction running beside it waited for it to end and then
     // delayed this frame's own reconstruction (pipelined latency p50 10-12 ms against a 5.6 ms frame).
@@ -1067,6 +1100,7 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     if (c->pipeline_mode == FR_PIPELINE_LATENCY && (c->recon_chains & 1)) {
       hipEventRecord(c->ev_jfa[c->slot], c->stream3);
       c->jfa_pending[c->slot] = true;
+      if (c->lat_arm) hipEventRecord(c->lat_ev[c->slot][2], c->stream3);
     }
     if ((c->recon_chains & 1) && (rc = enqueue_sibson(c, c->stream3))) return rc;
     if (t) hipEventRecord(ev[22], c->stream3);
@@ -1081,6 +1115,11 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     hipStreamWaitEvent(c->stream3, ev[17], 0);
     hipEventRecord(c->ev_recon[c->slot], c->stream3);  // this slot's buffers are free again after this
     c->recon_pending[c->slot] = true;
+    if (c->lat_arm && (c->recon_chains & 1)) {
+      hipEventRecord(c->lat_ev[c->slot][3], c->stream3);
+      c->lat_rec[c->slot] = true;
+    }
+    c->lat_arm = false;
     if (c->fc_cur >= 0) {  // fr_frame_clock: both chains of this frame are done
       hipEventRecord(c->fc_ev[c->fc_cur][1], c->stream3);
       c->fc_cur = -1;

@@ -26,8 +26,9 @@ size_t shade_counter_words();
 size_t shade_fx_slots(uint32_t max_active, int spp, uint32_t handoff);
 void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
 void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
-                     const f4*, f4*, uint8_t*, const uint8_t*, unsigned long long*, uint32_t*, int, uint8_t*, bool,
-                     uint32_t*, hipStream_t);
+                     const f4*, f4*, uint8_t*, const uint8_t*, unsigned long long*, uint32_t*, int, uint8_t*, uint32_t*,
+                     bool, uint32_t*, hipStream_t);
+size_t logpolar_inv_words(int W, int H);
 void launch_owner_counts(const FrameUniforms&, const uint32_t*, uint32_t*, hipStream_t);
 void launch_mask_words(const uint8_t*, const uint8_t*, int, int, unsigned long long*, uint32_t*, hipStream_t);
 void launch_compaction(int, int, const unsigned long long*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
@@ -126,6 +127,11 @@ struct fr_ctx {
   // latency mode: the end of the slot's JumpFlooding (or of its trace half when the chain is not run here)
   hipEvent_t ev_jfa[MAX_SLOTS] = {};
   bool jfa_pending[MAX_SLOTS] = {};
+  // latency mode's schedule: per slot, timing events at the front stages' start and end, the JumpFlooding's
+  // end and the reconstruction's end; the last completed frame's front and Sibson (JFA end -> end) times
+  hipEvent_t lat_ev[MAX_SLOTS][4] = {};
+  bool lat_rec[MAX_SLOTS] = {}, lat_arm = false;
+  float lat_front_ms = 0.0f, lat_sib_ms = 0.0f;
   // Tile sharding (fr_set_shard_plan): tile -> (owner << 24 | index among the owner's tiles) on the
   // device (FrameUniforms::shard_map), and the owners on the host. With sharding on, the front stages
   // also count every rank's active pixels from the unfolded mask (bcount per 16x16 block ->
@@ -180,6 +186,7 @@ struct fr_ctx {
   uint8_t* mask = nullptr;  // mask_p[slot]
   uint8_t* gclass = nullptr;
   uint8_t* lp_cache = nullptr;  // log-polar mask for (lp_gaze, lp_mode); recomputed when either changes
+  uint32_t* lp_inv = nullptr;   // the inverse log-polar map of every (u, v) of that gaze (k_logpolar_inv)
   f2 lp_gaze{-1e30f, -1e30f};
   int lp_mode = -1;
   unsigned long long* words = nullptr;

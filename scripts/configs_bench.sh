@@ -14,7 +14,7 @@ run C2 --scene bunny --width 1920 --height 1080 --spp 4 --dmd 1 --mask logpolar1
 run C3 --no-cpu-baseline
 # C3 with an eye-tracked gaze (the log-polar mask recomputed each frame): the full cursor circle (360 timed
 # frames, one degree each), and saccades (90 degrees every 30 frames); frame_clock_pipelined has p50/p99/max
-run C3gaze --no-cpu-baseline --gaze-path circle --steps 360 --warmup 5
-run C3sacc --no-cpu-baseline --gaze-path saccade --steps 360 --warmup 5
+run C3gaze --no-cpu-baseline --gaze-path circle --steps 360 --warmup 5 --serial-frames 360
+run C3sacc --no-cpu-baseline --gaze-path saccade --steps 360 --warmup 5 --serial-frames 360
 run C4 --no-cpu-baseline --scene vokselia --spp 8 --dmd 1 --mask saliency
 run C5 --no-cpu-baseline --scene vokselia --spp 8 --dmd 3 --mask saliency

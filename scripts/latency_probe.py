@@ -1,0 +1,23 @@
+"""Frames of the bench workload (C3: bunny 4K, 4 spp, GI 3, signed log-polar) in one pipeline mode, for a
+kernel trace: latency_probe.py [latency|throughput] [frames] [circle start degree]"""
+import numpy as np
+import os
+import sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'foveated-rendering-using-ray-tracing_amd'))
+import fovrt
+mode = sys.argv[1] if len(sys.argv) > 1 else "latency"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+t = fovrt.PathTracer(fovrt.Config(width=3840, height=2160, scene=1, mask_mode=4, spp=4, diffuse_max_depth=3))
+t.initialize()
+cam = fovrt.Camera.preset(1, 3840, 2160)
+t.update_optix_variables(cam)
+t.set_pipeline_mode(fovrt.PIPELINE_LATENCY if mode == "latency" else fovrt.PIPELINE_THROUGHPUT)
+circle = float(sys.argv[3]) if len(sys.argv) > 3 else None
+for f in range(n):
+    if circle is not None:  # bench.py --gaze-path circle: one degree per frame
+        a = np.deg2rad(circle + f)
+        t.set_gaze(1920 + 0.25 * 2160 * np.cos(a), (1080 + 0.25 * 2160 * np.sin(a)) / 1.25)
+    t.frame(timing=False)
+t.synchronize()
+print("done", mode, n)
+t.destroy()
