@@ -16,7 +16,8 @@ for f in sorted(glob.glob("gpurun_out/cfg_C*.log")):
            "ms_per_step": d["ms_per_step"], "stages_ms": {k: v["ms"] for k, v in d["stages"].items()},
            "megakernel_ms": d["roofline"].get("megakernel_ms"), "gaze": c.get("gaze"),
            "frame_ms_serial": d.get("frame_ms_serial"), "fps_serial": d.get("fps_serial"),
-           "frame_clock_pipelined": d.get("frame_clock_pipelined"), "steps": d.get("steps")}
+           "frame_clock_pipelined": d.get("frame_clock_pipelined"), "steps": d.get("steps"),
+           "fps_serial_mean": d.get("fps_serial_mean"), "pipeline_latency_mode": d.get("pipeline_latency_mode")}
     if "cpu_baseline" in d:
         row["cpu_baseline"] = {k: d["cpu_baseline"][k] for k in ("value", "unit", "cores", "kind", "fps")}
     out.append(row)
