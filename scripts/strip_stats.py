@@ -31,7 +31,7 @@ for ang in [float(a) for a in sys.argv[1:]] or [90.0, 180.0]:
     for s, r in zip(sid[big], rows[big]):
         strip_rows[s] = max(strip_rows.get(s, 0.0), r)
     its = np.array(sorted(strip_rows.values(), reverse=True)) / 4.0
-    lanes = np.array([(sid[big] == s).sum() for s in list(strip_rows)[:0]])
+    lane_eff = rows[big].sum() / max(64.0 * sum(strip_rows.values()), 1.0)  # lane-rows used / lane-rows issued
     # greedy: blocks claim strips in list order (the list is in k_sibson_runs' completion order; take the
     # descending order as the best case and a random order as the typical one)
     def makespan(order, nb=1024):
@@ -42,6 +42,7 @@ for ang in [float(a) for a in sys.argv[1:]] or [90.0, 180.0]:
     rng = np.random.default_rng(0)
     print(f"gaze {ang}: big pixels {int(big.sum())}, strips {len(its)}, iterations per strip max {its.max():.0f} "
           f"mean {its.mean():.1f}, total {its.sum():.0f}; makespan (1024 blocks) desc {makespan(its):.0f} "
-          f"random {makespan(rng.permutation(its)):.0f}; mean big-lanes per strip {big.sum() / max(len(its), 1):.1f}",
+          f"random {makespan(rng.permutation(its)):.0f}; mean big-lanes per strip {big.sum() / max(len(its), 1):.1f}; "
+          f"lane efficiency {lane_eff:.2f}",
           flush=True)
 t.destroy()
