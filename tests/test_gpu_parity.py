@@ -421,6 +421,48 @@ def test_sibson_strip_kernel_whole_image(fovrt_mod, oracle, W, H, kind, monkeypa
     assert np.abs(outs["0"] - sf).max() <= SIB_RUN_MAX, np.abs(outs["0"] - sf).max()
 
 
+@pytest.mark.parametrize("side", ["right", "left"])
+def test_sibson_strip_kernel_binade_classes(fovrt_mod, side, monkeypatch):
+    """k_sibson_strip on discs that span the whole row: seeds in one border column of a 3000 x 96 frame (W not a
+    power of two, so the tap step differs from 1/W by a different rounding in every binade of x = 2^-k). Seeds on
+    the right: the big discs sit at the left, and their rows cross a dozen segments near x = 0 (the class tables,
+    the merged runs, the left border tap). Seeds on the left: the discs run into the right border (the right
+    border tap) inside one binade. Against the shader's per-pixel loops on sampled pixels, and every pixel against
+    the k_sibson_wide form (FOVRT_SIB_STRIP=0) within one GL_LINEAR weight step."""
+    W, H = 3000, 96
+    m = np.zeros((H, W), np.uint8)
+    m[::6, W - 1 if side == "right" else 0] = 1
+    img = sparse_image(W, H, m, seed=17 if side == "right" else 19)
+    ex = _box_tracer(fovrt_mod, W, H)
+    ex.write(TN.SHADING, img)
+    fovrt_mod.JumpFlooding(ex).render(TN.SHADING)
+    coord, color = ex.read(TN.JFA_COORD), ex.read(TN.JFA_COLOR)
+    outs = {}
+    for strip in ("1", "0"):
+        monkeypatch.setenv("FOVRT_SIB_STRIP", strip)
+        ru = make_tracer(fovrt_mod, W, H, scene=0, mask=3, sibson_mode=0)
+        ru.write(TN.JFA_COORD, coord)
+        ru.write(TN.JFA_COLOR, color)
+        fovrt_mod.SibsonInterpolation(ru).render()
+        outs[strip] = ru.read(TN.SIBSON)
+        if strip == "1":
+            assert _sibson_counts(fovrt_mod, ru)[0] > 0  # the strip kernel ran
+        ru.destroy()
+    sf = outs["1"]
+    assert np.isfinite(sf).all() and np.array_equal(outs["0"][..., 3], sf[..., 3])
+    assert np.abs(outs["0"] - sf).max() <= SIB_RUN_MAX, np.abs(outs["0"] - sf).max()
+    assert (rmse_per_channel(outs["0"], sf) <= SIB_RUN_RMSE).all(), rmse_per_channel(outs["0"], sf)
+    yy, xx = np.mgrid[0:H, 0:W]
+    d = np.hypot(coord[..., 0] - (xx + 0.5) / W, coord[..., 1] - (yy + 0.5) / H)
+    big = np.flatnonzero(d.ravel() * H > 64)
+    assert big.size > 1000
+    for p in np.random.default_rng(7).choice(big, 12, replace=False):
+        y, x = divmod(int(p), W)
+        ref = _sibson_pixel_np(coord, color, x, y)
+        assert ref is not None and sf[y, x, 3] == 1.0
+        assert np.abs(sf[y, x, :3] - ref).max() <= SIB_RUN_MAX, (x, y, sf[y, x, :3], ref)
+
+
 def _sibson_pixel_np(coord, color, x, y):
     """One pixel of sibsonFS.glsl:16-49 in numpy: the shader's f32 position sequences (h, w += 1/size)
     walked in order, the taps outside [0, 1) or the disc dropped, GL_LINEAR + REPEAT at each tap
