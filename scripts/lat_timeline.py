@@ -7,7 +7,7 @@ import sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 ev = [(r["Kernel_Name"].split("(")[0].replace("void ", "").replace("fr::", ""), int(r["Start_Timestamp"]) / 1e6,
        int(r["End_Timestamp"]) / 1e6) for r in rows]
-starts = [i for i, e in enumerate(ev) if e[0] == "k_gbuffer"]
+starts = [i for i, e in enumerate(ev) if e[0].startswith("k_gbuffer")]
 print("frame  gbuf_end  mk_start  mk_end  jfa_start  sib_start  sib_end  atrous_end  | mk_ms sib_ms")
 prev = None
 for n, i in enumerate(starts):
@@ -27,7 +27,7 @@ for n, i in enumerate(starts):
     sr = first("k_sibson_runs", jf[2] if jf else mk[2])
     sib_end = max((e[2] for e in ev if e[0].startswith("k_sibson") and sr and sr[1] <= e[1] < sr[1] + 20.0
                    and (e[0] != "k_sibson_runs" or e is sr)), default=float("nan"))
-    at = [e for e in ev if e[0].startswith("k_atrous") and e[1] >= mk[2]][:3]
+    at = [e for e in ev if e[0].startswith("k_atrous") and e[1] >= mk[2]][:1]
     at_end = at[-1][2] if at else float("nan")
     rel = lambda x: x - t0
     print(f"{n:5d} {rel(g[2]):9.2f} {rel(mk[1]):9.2f} {rel(mk[2]):7.2f} {rel(jf[1]) if jf else float('nan'):10.2f} "
