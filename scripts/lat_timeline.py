@@ -25,8 +25,13 @@ for n, i in enumerate(starts):
         break
     jf = first("k_jfa_init", mk[2])
     sr = first("k_sibson_runs", jf[2] if jf else mk[2])
-    sib_end = max((e[2] for e in ev if e[0].startswith("k_sibson") and sr and sr[1] <= e[1] < sr[1] + 20.0
-                   and (e[0] != "k_sibson_runs" or e is sr)), default=float("nan"))
+    # this frame's Sibson: its k_sibson_runs and the Sibson kernels after it, up to the next k_sibson_runs
+    sib_end = float("nan")
+    if sr:
+        k = ev.index(sr)
+        sib = [sr] + [e for e in ev[k + 1:] if e[0].startswith("k_sibson")]
+        nxt = next((m for m, e in enumerate(sib[1:], 1) if e[0] == "k_sibson_runs"), len(sib))
+        sib_end = max(e[2] for e in sib[:nxt])
     at = [e for e in ev if e[0].startswith("k_atrous") and e[1] >= mk[2]][:1]
     at_end = at[-1][2] if at else float("nan")
     rel = lambda x: x - t0

@@ -13,7 +13,7 @@ cam = fovrt.Camera.preset(1, 3840, 2160)
 t.update_optix_variables(cam)
 t.set_pipeline_mode(fovrt.PIPELINE_LATENCY if mode == "latency" else fovrt.PIPELINE_THROUGHPUT)
 circle = float(sys.argv[3]) if len(sys.argv) > 3 else None
-for f in range(n):
+for f in range(n):  # (circle: one degree per frame from the start angle)
     if circle is not None:  # bench.py --gaze-path circle: one degree per frame
         a = np.deg2rad(circle + f)
         t.set_gaze(1920 + 0.25 * 2160 * np.cos(a), (1080 + 0.25 * 2160 * np.sin(a)) / 1.25)
