@@ -1026,21 +1026,32 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
       while ((e = hipEventQuery(w)) == hipErrorNotReady) {
       }
       if (e != hipSuccess) return fail(c, FR_E_HIP, std::string("frame failed: ") + hipGetErrorString(e));
-      // Just in time: the front stages should end when the previous frame's Sibson does (its path trace
-      // waits for both). A completed frame's times estimate the two; when its Sibson took longer than its
-      // front stages, the host waits the difference more (an eye-tracked gaze's big discs: 2-5 ms of
+      // Just in time: the front stages should end about when the previous frame's Sibson does (its path
+      // trace waits for both). A completed frame's times estimate the two; when its Sibson took longer than
+      // half its front stages, the host waits the difference more (an eye-tracked gaze's big discs: 2-5 ms of
       // Sibson against ~1.3 ms of front stages), so the gaze is sampled that much later.
       for (int k = 0; k < c->nslots; k++) {
         if (!c->lat_rec[k] || hipEventQuery(c->lat_ev[k][3]) != hipSuccess) continue;
         float f = 0.0f, sb = 0.0f;
         if (hipEventElapsedTime(&f, c->lat_ev[k][0], c->lat_ev[k][1]) == hipSuccess &&
             hipEventElapsedTime(&sb, c->lat_ev[k][2], c->lat_ev[k][3]) == hipSuccess) {
+          // The front stages' span is the smallest of the last eight: a front stage that overlapped the
+          // previous Sibson ran slower, and estimating from it started the next front stages earlier still (into
+          // more of that Sibson: a feedback that held the eye-tracked circle's fronts at ~4 ms instead of ~1)
+          c->lat_front_hist[c->lat_front_n++ & 7] = f;
           c->lat_front_ms = f;
+          for (int j = 1; j < std::min(8, c->lat_front_n); j++)
+            c->lat_front_ms = std::min(c->lat_front_ms, c->lat_front_hist[(c->lat_front_n - 1 - j) & 7]);
           c->lat_sib_ms = sb;
         }
         c->lat_rec[k] = false;
       }
-      const float delay_ms = c->jfa_pending[prev] ? c->lat_sib_ms - c->lat_front_ms : 0.0f;
+      // Only half of the front stages' span is overlapped: the big discs' strip kernel fills every CU, and a
+      // front stage started further into it ran ~4 ms instead of ~1, with its gaze sampled that much earlier
+      // (eye-tracked circle latency p99 16.2 -> 12.6 ms at 142 fps; C3 p50 6.15 -> 5.81 ms; overlapping none:
+      // p99 12.5 ms at 139 fps, the serial loop's rate). FOVRT_LAT_OVERLAP: the percentage (A/B knob).
+      static const float ovl = [] { const char* v = getenv("FOVRT_LAT_OVERLAP"); return v ? atoi(v) / 100.0f : 0.5f; }();
+      const float delay_ms = c->jfa_pending[prev] ? c->lat_sib_ms - ovl * c->lat_front_ms : 0.0f;
       if (delay_ms > 0.05f) {
         const auto t0 = std::chrono::steady_clock::now();
         while (std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count() < delay_ms &&

@@ -132,6 +132,8 @@ struct fr_ctx {
   hipEvent_t lat_ev[MAX_SLOTS][4] = {};
   bool lat_rec[MAX_SLOTS] = {}, lat_arm = false;
   float lat_front_ms = 0.0f, lat_sib_ms = 0.0f;
+  float lat_front_hist[8] = {};  // the last frames' front-stage spans: their minimum is the uncontended one
+  int lat_front_n = 0;
   // Tile sharding (fr_set_shard_plan): tile -> (owner << 24 | index among the owner's tiles) on the
   // device (FrameUniforms::shard_map), and the owners on the host. With sharding on, the front stages
   // also count every rank's active pixels from the unfolded mask (bcount per 16x16 block ->
