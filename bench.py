@@ -189,6 +189,26 @@ def load_traffic(kernels, config):
     return None, None
 
 
+def load_issue(kernel, config):
+    """The SIMD issue picture of `kernel` from the newest profiles/*_pmc_issue.json recorded on the same
+    workload (scripts/pmc_sq.sh + scripts/pmc_issue.py), else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_issue.json")), reverse=True):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        cfg = doc.get("config") or {}
+        if any(cfg.get(k) != config.get(k) for k in ("scene", "width", "height", "spp", "diffuse_max_depth",
+                                                     "mask_mode")):
+            continue
+        ent = doc.get("kernels", {}).get(kernel)
+        if ent:
+            return dict(ent, source=os.path.relpath(path, ROOT))
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -550,6 +570,10 @@ def main():
         result["roofline"]["traffic"] = int(traffic)
         result["roofline"]["traffic_source"] = src
         result["roofline"]["measured_hbm_GBs"] = round(traffic / (launch_ms * 1e-3) / 1e9, 1)
+    issue = load_issue("k_shade_paths", result["config"]) if R == 1 else None
+    if issue is not None:
+        # what bounds the megakernel instead of HBM: the SIMD's VALU issue (profiles/*_pmc_issue.json)
+        result["roofline"]["issue"] = issue
     if group:
         group.destroy()
     # the GPU BVH builder on this scene (after every measurement: it replaces the BVH)
