@@ -378,7 +378,7 @@ def _sibson_counts(fovrt_mod, t):
 
 @pytest.mark.parametrize("W,H,kind", [(640, 360, "logpolar180"), (512, 288, "few"), (256, 160, "corner")])
 def test_sibson_strip_kernel_whole_image(fovrt_mod, oracle, W, H, kind, monkeypatch):
-    """k_sibson_strip (the default for discs over 2 x 32 rows) on whole images against the oracle's per-tap
+    """k_sibson_strip (the default for discs over 2 x 24 rows) on whole images against the oracle's per-tap
     Sibson (sibsonFS.glsl:16-49), every pixel: an off-centre signed log-polar mask (bench.py --gaze-path's
     cursor at 180 degrees, scaled to 640 x 360), a few-seed frame and two corner seeds. The pass must list
     strips (fr__sibson_counts), and the k_sibson_wide form (FOVRT_SIB_STRIP=0) of the same JFA output must
