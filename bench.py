@@ -572,8 +572,12 @@ def main():
         result["roofline"]["measured_hbm_GBs"] = round(traffic / (launch_ms * 1e-3) / 1e9, 1)
     issue = load_issue("k_shade_paths", result["config"]) if R == 1 else None
     if issue is not None:
-        # what bounds the megakernel instead of HBM: the SIMD's VALU issue (profiles/*_pmc_issue.json)
+        # what bounds the megakernel instead of HBM: the SIMD's VALU issue (profiles/*_pmc_issue.json). It comes
+        # from a separate counter pass (an earlier run, possibly of an earlier build), never from this run
+        issue["measured_in_this_run"] = False
         result["roofline"]["issue"] = issue
+    if traffic is not None:
+        result["roofline"]["traffic_measured_in_this_run"] = False
     if group:
         group.destroy()
     # the GPU BVH builder on this scene (after every measurement: it replaces the BVH)

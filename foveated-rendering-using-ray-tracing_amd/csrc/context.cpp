@@ -15,6 +15,30 @@
 
 #include <chrono>
 #include "ctx_internal.h"
+#include <immintrin.h>
+#include <sched.h>
+
+namespace {
+// Host-side waits of the latency mode poll (a blocking wait woke the host up to milliseconds late). The spin
+// pauses between queries, yields the core every 64 polls (RCCL proxy threads or other ranks' host threads may
+// share it), and gives up after a deadline instead of spinning forever on an event that never completes.
+constexpr float kPollDeadlineMs = 10000.0f;
+inline void cpu_relax() { _mm_pause(); }
+hipError_t poll_event(hipEvent_t ev, float deadline_ms) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t n = 1;; n++) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+    if ((n & 63u) == 0) {
+      if (std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count() > deadline_ms)
+        return hipErrorNotReady;
+      sched_yield();
+    } else {
+      cpu_relax();
+    }
+  }
+}
+}  // namespace
 
 using namespace fr;
 
@@ -497,7 +521,9 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     std::string werr;
     if (!bvh_builder_warm(c->bvh_work, c->stream, werr)) { c->err = werr; return bail(FR_E_HIP); }
   }
-  if (hipDeviceSynchronize() != hipSuccess) { c->err = "device synchronisation (scene) failed"; return bail(FR_E_HIP); }
+  // (the uploads above are synchronous hipMemcpy calls; the builder warm-up ran on c->stream: wait for this
+  // context's stream only, not for other contexts or groups rendering on the device)
+  if (hipStreamSynchronize(c->stream) != hipSuccess) { c->err = "stream synchronisation (scene) failed"; return bail(FR_E_HIP); }
   DevScene& d = c->dsc;
   memset(&d, 0, sizeof(d));
   d.nodes = c->d_nodes; d.tri_geo = c->d_tri; d.tri_prim = c->d_prim; d.shade = c->d_shade;
@@ -1023,9 +1049,9 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
       // (polled: a blocking wait woke the host up to milliseconds late, and the GPU idled meanwhile)
       hipEvent_t w = c->jfa_pending[prev] ? c->ev_jfa[prev] : c->ev_trace[prev];
       hipError_t e;
-      while ((e = hipEventQuery(w)) == hipErrorNotReady) {
-      }
-      if (e != hipSuccess) return fail(c, FR_E_HIP, std::string("frame failed: ") + hipGetErrorString(e));
+      if ((e = poll_event(w, kPollDeadlineMs)) != hipSuccess)
+        return fail(c, FR_E_HIP, e == hipErrorNotReady ? std::string("frame failed: the previous frame did not complete within the poll deadline")
+                                                        : std::string("frame failed: ") + hipGetErrorString(e));
       // Just in time: the front stages should end about when the previous frame's Sibson does (its path
       // trace waits for both). A completed frame's times estimate the two; when its Sibson took longer than
       // half its front stages, the host waits the difference more (an eye-tracked gaze's big discs: 2-5 ms of
@@ -1056,6 +1082,7 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
         const auto t0 = std::chrono::steady_clock::now();
         while (std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count() < delay_ms &&
                hipEventQuery(c->ev_recon[prev]) == hipErrorNotReady) {
+          cpu_relax();
         }
       }
       c->jfa_pending[prev] = false;
@@ -1512,6 +1539,120 @@ int fr_write_buffer(fr_ctx* c, int id, const void* host, size_t bytes) {
     c->compacted = false;
     c->mask_dirty = true;
   }
+  return FR_OK;
+}
+
+// ---- Snapshot / restore of the temporal state (deterministic multi-frame golden tests) ----
+// What a frame carries into the next one: the history and depth ping-pong pairs (FR/PathTracer.cpp:226-238),
+// the pull / push atlases and the push pass's snapshot texels (the push reads the previous frame's atlas,
+// FR/PullPushInterpolation.cpp:57-58), the m_accumFrame counter with its pending light reset, the light
+// emission, and the camera / gaze uniforms of the last update. Everything else a frame reads it writes first.
+// Layout: a fixed header, then the buffers in the order below (cache before current of each pair).
+namespace {
+constexpr uint32_t kSnapMagic = 0x4E535246u;  // "FRSN"
+constexpr uint32_t kSnapVersion = 1;
+struct SnapHeader {
+  uint32_t magic, version;
+  int32_t width, height, pp_S, spp, scene, mask_mode;
+  uint32_t accum, light_pending;
+  float light_emission[3];
+  int32_t diffuse_max_depth;
+  float inv_vp[16], prev_vp[16], eye[3], prev_eye[3], gaze[2];
+  uint64_t payload_bytes;
+};
+struct SnapPart {
+  void* dev;
+  size_t bytes;
+};
+constexpr int kSnapParts = 7;
+struct SnapParts {
+  SnapPart p[kSnapParts];
+  const SnapPart* begin() const { return p; }
+  const SnapPart* end() const { return p + kSnapParts; }
+};
+SnapParts snap_parts(fr_ctx* c) {
+  const size_t img = (size_t)c->W * c->H * sizeof(f4);
+  const size_t atlas = (size_t)c->pp_S * (c->pp_S + c->pp_S / 2) * sizeof(f4);
+  return SnapParts{{{c->img[c->hist_cache], img}, {c->img[c->hist_cur], img}, {c->img[c->depth_cache], img},
+                    {c->img[c->depth_cur], img}, {c->pull, atlas}, {c->push, atlas},
+                    {c->snap, pp_snap_count(c->pp_S) * sizeof(f4)}}};
+}
+size_t snap_total(fr_ctx* c) {
+  size_t n = sizeof(SnapHeader);
+  for (const SnapPart& p : snap_parts(c)) n += p.bytes;
+  return n;
+}
+}  // namespace
+
+int fr_snapshot_bytes(fr_ctx* c, size_t* bytes) {
+  if (!c || !bytes) return FR_E_INVALID;
+  *bytes = snap_total(c);
+  return FR_OK;
+}
+
+int fr_snapshot(fr_ctx* c, void* host, size_t bytes) {
+  if (!c) return FR_E_INVALID;
+  const size_t need = snap_total(c);
+  if (!host || bytes < need) return fail(c, FR_E_INVALID, "snapshot: buffer smaller than fr_snapshot_bytes");
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  SnapHeader h{};
+  h.magic = kSnapMagic; h.version = kSnapVersion;
+  h.width = c->W; h.height = c->H; h.pp_S = c->pp_S; h.spp = c->U.spp; h.scene = c->cfg.scene;
+  h.mask_mode = c->U.mask_mode;
+  h.accum = c->accum; h.light_pending = c->light_pending ? 1u : 0u;
+  h.light_emission[0] = c->dsc.light_emission.x; h.light_emission[1] = c->dsc.light_emission.y;
+  h.light_emission[2] = c->dsc.light_emission.z;
+  h.diffuse_max_depth = c->U.diffuse_max_depth;
+  memcpy(h.inv_vp, &c->U.inv_vp, sizeof(h.inv_vp));
+  memcpy(h.prev_vp, &c->U.prev_vp, sizeof(h.prev_vp));
+  memcpy(h.eye, &c->U.eye, sizeof(h.eye));
+  memcpy(h.prev_eye, &c->U.prev_eye, sizeof(h.prev_eye));
+  memcpy(h.gaze, &c->U.gaze, sizeof(h.gaze));
+  h.payload_bytes = need - sizeof(SnapHeader);
+  char* out = static_cast<char*>(host);
+  memcpy(out, &h, sizeof(h));
+  size_t off = sizeof(h);
+  for (const SnapPart& p : snap_parts(c)) {
+    HIP_TRY(c, hipMemcpyAsync(out + off, p.dev, p.bytes, hipMemcpyDeviceToHost, c->stream));
+    off += p.bytes;
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FR_OK;
+}
+
+int fr_restore(fr_ctx* c, const void* host, size_t bytes) {
+  if (!c) return FR_E_INVALID;
+  const size_t need = snap_total(c);
+  if (!host || bytes < need) return fail(c, FR_E_INVALID, "restore: buffer smaller than fr_snapshot_bytes");
+  SnapHeader h;
+  memcpy(&h, host, sizeof(h));
+  if (h.magic != kSnapMagic || h.version != kSnapVersion) return fail(c, FR_E_INVALID, "restore: not a fovrt snapshot");
+  if (h.width != c->W || h.height != c->H || h.pp_S != c->pp_S || h.spp != c->U.spp || h.scene != c->cfg.scene ||
+      h.payload_bytes != need - sizeof(SnapHeader))
+    return fail(c, FR_E_INVALID, "restore: snapshot of another configuration (size, spp or scene differ)");
+  join_recon(c);
+  hipSetDevice(c->cfg.device);
+  const char* in = static_cast<const char*>(host);
+  size_t off = sizeof(h);
+  for (const SnapPart& p : snap_parts(c)) {
+    HIP_TRY(c, hipMemcpyAsync(p.dev, in + off, p.bytes, hipMemcpyHostToDevice, c->stream));
+    off += p.bytes;
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->accum = h.accum;
+  c->light_pending = h.light_pending != 0;
+  c->dsc.light_emission = mk3(h.light_emission[0], h.light_emission[1], h.light_emission[2]);
+  c->U.diffuse_max_depth = h.diffuse_max_depth;
+  c->U.mask_mode = h.mask_mode;
+  memcpy(&c->U.inv_vp, h.inv_vp, sizeof(h.inv_vp));
+  memcpy(&c->U.prev_vp, h.prev_vp, sizeof(h.prev_vp));
+  memcpy(&c->U.eye, h.eye, sizeof(h.eye));
+  memcpy(&c->U.prev_eye, h.prev_eye, sizeof(h.prev_eye));
+  memcpy(&c->U.gaze, h.gaze, sizeof(h.gaze));
+  c->lp_gaze = f2{-1e30f, -1e30f};  // the log-polar mask cache is recomputed for the restored gaze
+  c->lp_mode = -1;
+  c->sib_prefix_fresh = false;
   return FR_OK;
 }
 

@@ -164,6 +164,9 @@ _SIGS = {
     "fr_read_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_write_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
     "fr_copy_buffer": [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t],
+    "fr_snapshot_bytes": [C.c_void_p, C.POINTER(C.c_size_t)],
+    "fr_snapshot": [C.c_void_p, C.c_void_p, C.c_size_t],
+    "fr_restore": [C.c_void_p, C.c_void_p, C.c_size_t],
     "fr_rebuild_bvh": [C.c_void_p, C.POINTER(C.c_float)],
     "fr_set_positions": [C.c_void_p, C.POINTER(C.c_float), C.c_size_t],
     "fr_get_stats": [C.c_void_p, C.POINTER(fr_stats)],
@@ -541,6 +544,19 @@ class PathTracer:
         """The reconstruction half of a frame (JFA -> Sibson -> pull-push -> A-Trous)."""
         return self._frame(_lib.fr_reconstruct_frame, timing)
 
+    def snapshot(self) -> bytes:
+        """fr_snapshot: the temporal state (history / depth pairs, pull-push atlases, frame counter, camera)."""
+        n = C.c_size_t()
+        self._check(_lib.fr_snapshot_bytes(self._ctx, C.byref(n)))
+        buf = (C.c_uint8 * n.value)()
+        self._check(_lib.fr_snapshot(self._ctx, buf, n.value))
+        return bytes(buf)
+
+    def restore(self, snap: bytes):
+        """fr_restore: load a snapshot of a context with the same size, spp and scene."""
+        buf = (C.c_uint8 * len(snap)).from_buffer_copy(snap)
+        self._check(_lib.fr_restore(self._ctx, buf, len(snap)))
+
     def copy_buffer(self, buffer_id, device_ptr, nbytes):
         """Device-to-device copy of a buffer into memory the caller owns (e.g. a torch tensor)."""
         self._check(_lib.fr_copy_buffer(self._ctx, int(buffer_id), C.c_void_p(device_ptr), int(nbytes)))
@@ -883,6 +899,13 @@ class Group:
             if self._owns_comm and self._comm is not None:
                 _lib.fr_rccl_comm_destroy(self._comm)
                 self._comm = None
+        # break the tracer <-> group reference cycle: after an explicit destroy both sides are freed by
+        # reference counting again (their GPU memory no longer waits for the cycle collector)
+        for t in getattr(self, "tracers", ()):
+            gs = getattr(t, "_groups", None)
+            if gs is not None and self in gs:
+                gs.remove(self)
+        self.tracers = []
 
     def __del__(self):
         self.destroy()

@@ -391,6 +391,16 @@ int fr_get_buffer(fr_ctx* ctx, int id, fr_buffer_view* view);
 int fr_read_buffer(fr_ctx* ctx, int id, void* host, size_t bytes);
 int fr_write_buffer(fr_ctx* ctx, int id, const void* host, size_t bytes);
 int fr_copy_buffer(fr_ctx* ctx, int id, void* device_dst, size_t bytes);  /* device-to-device, synchronous */
+/* Snapshot / restore of the temporal state a frame hands to the next (the reference keeps it in
+ * the history / depth ping-pong, FR/PathTracer.cpp:226-238, and in the push atlas carried across frames,
+ * FR/PullPushInterpolation.cpp:57-58): HISTORY_CACHE / HISTORY, DEPTH_CACHE / DEPTH, the pull and push atlases
+ * and the push snapshot texels, m_accumFrame (with a pending light reset), the light emission, the diffuse
+ * depth and the last camera / gaze uniforms. fr_snapshot_bytes gives the size; fr_snapshot copies it to host
+ * memory after all pending work; fr_restore loads it into a context of the same size, spp and scene
+ * (FR_E_INVALID otherwise), so the next frame equals the one that followed the snapshot, bit for bit. */
+int fr_snapshot_bytes(fr_ctx* ctx, size_t* bytes);
+int fr_snapshot(fr_ctx* ctx, void* host, size_t bytes);
+int fr_restore(fr_ctx* ctx, const void* host, size_t bytes);
 
 int fr_get_stats(fr_ctx* ctx, fr_stats* stats);
 int fr_reset_stats(fr_ctx* ctx);

@@ -182,6 +182,15 @@ class PathTracer {
     return v;
   }
   fr_stats stats() { fr_stats s{}; check(fr_get_stats(ctx(), &s), ctx_, "stats"); return s; }
+  // temporal state (history / depth pairs, pull-push atlases, m_accumFrame, camera) to host memory and back
+  std::vector<uint8_t> snapshot() {
+    size_t n = 0;
+    check(fr_snapshot_bytes(ctx(), &n), ctx_, "snapshot");
+    std::vector<uint8_t> v(n);
+    check(fr_snapshot(ctx(), v.data(), v.size()), ctx_, "snapshot");
+    return v;
+  }
+  void restore(const std::vector<uint8_t>& v) { check(fr_restore(ctx(), v.data(), v.size()), ctx_, "restore"); }
   // live per-launch HIP-event timing of the shading stage (off by default)
   void kernel_timing(bool on) { check(fr_kernel_timing(ctx(), on ? 1 : 0), ctx_, "kernel_timing"); }
   fr_stage_times kernel_times() { fr_stage_times t{}; check(fr_kernel_times(ctx(), &t), ctx_, "kernel_times"); return t; }

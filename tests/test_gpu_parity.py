@@ -6,6 +6,8 @@ equality; stages whose arithmetic goes through the platform fp32 libm (the mater
 max-error bound. Each stage is fed the GPU's own upstream buffers, so a tolerance in one stage
 never leaks into the next stage's comparison.
 """
+import copy
+
 import numpy as np
 import pytest
 
@@ -1221,3 +1223,50 @@ def test_frame_clock_and_shard_count_state(fovrt_mod):
     with pytest.raises(fovrt_mod.FovrtError):
         t.shard_counts(3)
     t.destroy()
+
+
+def test_snapshot_restore_reproduces_next_frame(fovrt_mod):
+    """fr_snapshot / fr_restore: the temporal state a frame hands to the next (history and depth
+    ping-pong, FR/PathTracer.cpp:226-238; the pull-push atlases the push reads across frames,
+    FR/PullPushInterpolation.cpp:57-58; m_accumFrame; the camera) restored mid-sequence, into a fresh context
+    and into the same one after it ran on, reproduces the next frame bit for bit: camera panning, gaze moving."""
+    W, H = 320, 192
+    a = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    cam = fovrt_mod.Camera.preset(1, W, H)
+    gazes = [(W / 2 + 25 * np.cos(f), (H / 2 + 25 * np.sin(f)) / 1.25) for f in range(8)]
+
+    def advance(t, f):
+        t.update_optix_variables(cams[f])
+        t.set_gaze(*gazes[f])
+        t.frame(timing=False)
+
+    cams = []  # every frame's camera (with its previous pose), so a frame can be replayed
+    for f in range(8):
+        cam.setPrevState()
+        cam.lookAt(np.asarray(cam.target) + np.array([0.01, 0.005, 0.0], np.float32))
+        cams.append(copy.deepcopy(cam))
+    for f in range(4):
+        advance(a, f)
+    snap = a.snapshot()
+    advance(a, 4)
+    outs = (TN.SHADING, TN.HISTORY_CACHE, TN.DEPTH_CACHE, TN.JFA_COLOR, TN.SIBSON, TN.PULLPUSH, TN.ATROUS, TN.MASK)
+    want = {tid: a.read(tid) for tid in outs}
+    # a fresh context restored from the snapshot
+    b = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    b.restore(snap)
+    advance(b, 4)
+    for tid in outs:
+        assert equal_nan(b.read(tid), want[tid]), ("fresh context", tid)
+    # the same context, restored after two more frames
+    advance(a, 5)
+    advance(a, 6)
+    a.restore(snap)
+    advance(a, 4)
+    for tid in outs:
+        assert equal_nan(a.read(tid), want[tid]), ("same context", tid)
+    # a snapshot of another configuration is refused
+    c = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=2, dmd=3)
+    with pytest.raises(fovrt_mod.FovrtError):
+        c.restore(snap)
+    for t in (a, b, c):
+        t.destroy()
