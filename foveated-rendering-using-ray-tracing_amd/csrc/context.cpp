@@ -418,11 +418,30 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   const int p_recon = prio_mode == 1 ? lo : prio_mode == 2 ? hi : 0;
   const int p_front = prio_mode == 1 || prio_mode == 3 ? hi : prio_mode == 2 || prio_mode == 4 ? lo : 0;
   const int p_jfa = prio_mode == 4 ? hi : p_recon, p_pp = prio_mode == 4 ? lo : p_recon;
-  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, p_trace) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, p_pp) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, p_jfa) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, p_trace) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, p_front) != hipSuccess) {
+  // CU masks (FOVRT_RECON_CUS = R, A/B knob, 0 = off): the two reconstruction streams run on R CUs spread evenly
+  // over the device's CU mask (every XCD); FOVRT_CU_DISJOINT=1 also keeps the trace streams off those CUs.
+  static const int recon_cus = [] { const char* v = getenv("FOVRT_RECON_CUS"); return v ? atoi(v) : 0; }();
+  static const int cu_disjoint = [] { const char* v = getenv("FOVRT_CU_DISJOINT"); return v ? atoi(v) : 0; }();
+  int ncu = 0;
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg.device);
+  const bool masked = recon_cus > 0 && recon_cus < ncu;
+  std::vector<uint32_t> m_recon((size_t)(ncu + 31) / 32, 0u), m_trace((size_t)(ncu + 31) / 32, 0u);
+  if (masked) {
+    for (int i = 0; i < recon_cus; i++) {
+      const int b = (int)((int64_t)i * ncu / recon_cus);
+      m_recon[(size_t)b / 32] |= 1u << (b % 32);
+    }
+    for (int b = 0; b < ncu; b++)
+      if (!cu_disjoint || !(m_recon[(size_t)b / 32] & (1u << (b % 32)))) m_trace[(size_t)b / 32] |= 1u << (b % 32);
+  }
+  auto mk = [&](hipStream_t* st, int prio, bool recon) {
+    if (!masked) return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio);
+    std::vector<uint32_t>& m = recon ? m_recon : m_trace;
+    return hipExtStreamCreateWithCUMask(st, (uint32_t)m.size(), m.data());
+  };
+  if (mk(&c->stream, p_trace, false) != hipSuccess || mk(&c->stream2, p_pp, true) != hipSuccess ||
+      mk(&c->stream3, p_jfa, true) != hipSuccess || mk(&c->stream4, p_trace, false) != hipSuccess ||
+      mk(&c->stream5, p_front, false) != hipSuccess) {
     c->err = "stream create failed";
     return bail(FR_E_HIP);
   }
@@ -882,9 +901,9 @@ static int enqueue_jfa(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {
   int p;
   if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "jfa: bad input buffer");
   const bool run_form = c->cfg.sibson_mode == 0;
-  launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->ftab, c->W, c->H,
-             run_form ? c->sib_prefix : nullptr, run_form ? c->sib_blocks : nullptr,
-             stream ? stream : c->stream);
+  c->jfa_final = launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->ftab, c->W,
+                            c->H, run_form ? c->sib_prefix : nullptr, run_form ? c->sib_blocks : nullptr,
+                            stream ? stream : c->stream);
   c->sib_prefix_fresh = run_form;
   return check_launch(c);
 }
@@ -892,7 +911,7 @@ static int enqueue_sibson(fr_ctx* c, hipStream_t stream = nullptr) {
   if (c->cfg.sibson_mode == 1)  // per tap, bit-exact against the oracle
     launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, stream ? stream : c->stream);
   else  // run form (default): exact tap sets, rounding-level differences
-    launch_sibson_runs(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->sib_prefix, c->sib_blocks, c->sib_rowp, c->sib_wide,
+    launch_sibson_runs(c->img[P_JFA_COORD], c->jfa_final, c->img[P_JFA_COLOR], c->sib_prefix, c->sib_blocks, c->sib_rowp, c->sib_wide,
                        c->sib_strips, c->img[P_SIBSON], c->W, c->H, c->sib_prefix_fresh, c->sib_strip,
                        stream ? stream : c->stream);
   return check_launch(c);
@@ -962,9 +981,10 @@ int fr_logpolar_render(fr_ctx* c, int in_buffer, uint64_t* ns) {
   return ns_timed(c, [&] { return enqueue_logpolar(c, in_buffer); }, ns);
 }
 
+static int buffer_view(fr_ctx* c, int id, fr_buffer_view* v);
 int fr_copy_buffer(fr_ctx* c, int id, void* dst, size_t bytes) {
   fr_buffer_view v;
-  int rc = fr_get_buffer(c, id, &v);
+  int rc = buffer_view(c, id, &v);
   if (rc) return rc;
   if (!dst || bytes > v.bytes) return fail(c, FR_E_INVALID, "copy_buffer: size");
   hipSetDevice(c->cfg.device);
@@ -1495,6 +1515,14 @@ int fr_gaze_target(fr_ctx* c, float xyz[3]) {
 }
 
 int fr_get_buffer(fr_ctx* c, int id, fr_buffer_view* v) {
+  const int rc = buffer_view(c, id, v);
+  // the caller may write the JFA outputs through the view: Sibson then derives its seeds and row prefix sums
+  // from them again instead of from the JFA run's own state
+  if (rc == FR_OK && (id == FR_BUF_JFA_COLOR || id == FR_BUF_JFA_COORD)) c->sib_prefix_fresh = false;
+  return rc;
+}
+
+static int buffer_view(fr_ctx* c, int id, fr_buffer_view* v) {
   if (!c || !v) return FR_E_INVALID;
   join_recon(c);  // later work on the context stream is ordered after the reconstruction
   const size_t N = (size_t)c->W * c->H;
@@ -1518,7 +1546,7 @@ int fr_get_buffer(fr_ctx* c, int id, fr_buffer_view* v) {
 
 int fr_read_buffer(fr_ctx* c, int id, void* host, size_t bytes) {
   fr_buffer_view v;
-  int rc = fr_get_buffer(c, id, &v);
+  int rc = buffer_view(c, id, &v);
   if (rc) return rc;
   if (!host || bytes > v.bytes) return fail(c, FR_E_INVALID, "read_buffer: size");
   HIP_TRY(c, hipMemcpyAsync(host, v.device_ptr, bytes, hipMemcpyDeviceToHost, c->stream));
@@ -1528,12 +1556,13 @@ int fr_read_buffer(fr_ctx* c, int id, void* host, size_t bytes) {
 
 int fr_write_buffer(fr_ctx* c, int id, const void* host, size_t bytes) {
   fr_buffer_view v;
-  int rc = fr_get_buffer(c, id, &v);
+  int rc = buffer_view(c, id, &v);
   if (rc) return rc;
   if (!host || bytes > v.bytes) return fail(c, FR_E_INVALID, "write_buffer: size");
   HIP_TRY(c, hipMemcpyAsync(v.device_ptr, host, bytes, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  if (id == FR_BUF_JFA_COLOR) c->sib_prefix_fresh = false;  // Sibson's row prefix sums no longer match it
+  // Sibson's row prefix sums (and the JFA state it reads its seeds from) no longer match these
+  if (id == FR_BUF_JFA_COLOR || id == FR_BUF_JFA_COORD) c->sib_prefix_fresh = false;
   if (id == FR_BUF_MASK) {
     // a host-written mask must also drive the compaction: rebuild the wave ballots from it
     c->compacted = false;

@@ -44,9 +44,10 @@ void launch_vring_pack(const f4*, int, int, int, const int32_t*, int, uint32_t*,
 void launch_vring_unpack(const uint32_t*, int, int, int, const int32_t*, int, f4*, hipStream_t);
 void launch_shard_unpack_active(const FrameUniforms&, const f4*, const uint32_t*, uint32_t, uint32_t, const f4*, const f4*, f4*,
                                 f4*, hipStream_t);
-void launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, f4*, f4*, hipStream_t);
+const u2* launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, f4*, f4*, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
-void launch_sibson_runs(const f4*, const f4*, f4*, f4*, f4*, uint32_t*, uint32_t*, f4*, int, int, bool, bool, hipStream_t);
+void launch_sibson_runs(const f4*, const u2*, const f4*, f4*, f4*, f4*, uint32_t*, uint32_t*, f4*, int, int, bool, bool,
+                        hipStream_t);
 int sibson_prefix_blocks(int W);
 size_t sibson_strip_words(int W, int H);
 size_t sibson_rowp_texels(int W, int H);
@@ -213,7 +214,9 @@ struct fr_ctx {
   uint32_t* sib_wide = nullptr;  // Sibson run form: wide-disc pixel lists (two counts, then W*H indices)
   uint32_t* sib_strips = nullptr;  // Sibson run form: k_sibson_strip's strip list and flags (sibson_strip_words)
   f4* sib_rowp = nullptr;          // Sibson strip kernel: whole-row prefix sums (sibson_rowp_texels)
-  bool sib_prefix_fresh = false;  // the last JFA wrote them with JFA_COLOR (cleared when JFA_COLOR is written)
+  bool sib_prefix_fresh = false;  // the last JFA wrote them with JFA_COLOR (cleared when JFA_COLOR / JFA_COORD are
+                                  // written or handed out, fr_get_buffer)
+  const u2* jfa_final = nullptr;  // that JFA's final state (the seeds k_sibson_runs reads while the prefix is fresh)
   int pp_S = 0;
   DevStats* stats = nullptr;
   FrameUniforms U;

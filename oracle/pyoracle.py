@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+# ORACLE_LIB: the sanitizer build (oracle/Makefile asan, scripts/asan_cpu_suite.sh)
+LIB = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 
 _lib = None
 F = C.POINTER(C.c_float)

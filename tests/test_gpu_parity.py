@@ -423,6 +423,44 @@ def test_sibson_strip_kernel_whole_image(fovrt_mod, oracle, W, H, kind, monkeypa
     assert np.abs(outs["0"] - sf).max() <= SIB_RUN_MAX, np.abs(outs["0"] - sf).max()
 
 
+@pytest.mark.parametrize("W,H,kind", [(201, 400, "rightedge"), (329, 250, "rightedge"), (640, 360, "logpolar180"),
+                                      (1920, 1080, "logpolar")])
+def test_sibson_seeds_from_jfa_state(fovrt_mod, oracle, W, H, kind):
+    """The run form right after its own JumpFlooding reads each pixel's seed from the final 8-byte JFA state
+    (k_sibson_runs<true>); after the JFA outputs were written (or handed out) it reads JFA_COORD instead. Both
+    must give the same image bit for bit. The right-edge cases put big discs (over 2 x 24 rows) in the last,
+    partial 16-pixel tile column (W % 16 = 9 and 9) away from the top and bottom rows, where lanes past the
+    tile's pixel count take part in the wave's row-range reduction."""
+    if kind == "rightedge":
+        m = np.zeros((H, W), np.uint8)
+        m[::16, ::16] = 1  # seeds everywhere (small discs) but in a hole at the right border's middle
+        m[H // 2 - 75:H // 2 + 75, W - 90:] = 0
+        m[H // 2 - 70, W - 1] = m[H // 2 + 70, W - 1] = 1
+    elif kind == "logpolar180":
+        m = logpolar_mask_np(W, H, W / 2 - 0.25 * H, H / 2, signed=True)
+    else:
+        m = logpolar_mask_np(W, H, W // 2, H - H // 2, signed=True)
+    img = sparse_image(W, H, m, seed=W * 5 + H)
+    t = make_tracer(fovrt_mod, W, H, scene=0, mask=3, sibson_mode=0)
+    t.write(TN.SHADING, img)
+    fovrt_mod.JumpFlooding(t).render(TN.SHADING)
+    fovrt_mod.SibsonInterpolation(t).render()  # seeds from the JFA state
+    a = t.read(TN.SIBSON)
+    coord, color = t.read(TN.JFA_COORD), t.read(TN.JFA_COLOR)
+    if kind == "rightedge":
+        assert _sibson_counts(fovrt_mod, t)[0] > 0  # big discs went to the strip kernel
+    t.write(TN.JFA_COORD, coord)  # (the same values: now from JFA_COORD)
+    fovrt_mod.SibsonInterpolation(t).render()
+    b = t.read(TN.SIBSON)
+    assert equal_nan(a, b), mismatch_report(a, b)
+    if W * H <= 640 * 360:
+        rs = oracle.sibson(coord, color)
+        assert np.isfinite(a).all() and np.array_equal(a[..., 3], rs[..., 3])
+        assert np.abs(a - rs).max() <= SIB_RUN_MAX, np.abs(a - rs).max()
+        assert (rmse_per_channel(a, rs) <= 2e-4).all(), rmse_per_channel(a, rs)
+    t.destroy()
+
+
 @pytest.mark.parametrize("side", ["right", "left"])
 def test_sibson_strip_kernel_binade_classes(fovrt_mod, side, monkeypatch):
     """k_sibson_strip on discs that span the whole row: seeds in one border column of a 3000 x 96 frame (W not a
