@@ -27,10 +27,11 @@ for ang in angles:
     for _ in range(2):
         tm = t.frame(True)
     t.synchronize()
+    # (timed before JFA_COORD is read: handing out a JFA output makes Sibson re-derive its seeds and prefix sums)
+    ms = np.median([si.render() / 1e6 for _ in range(5)])
     c = t.read(TN.JFA_COORD)
     d = np.sqrt((c[..., 0] - fx) ** 2 + (c[..., 1] - fy) ** 2)
     rows = 2 * d * H
-    ms = np.median([si.render() / 1e6 for _ in range(5)])
     print(f"gaze {ang}: rays {t.ray_count()} sibson_frame {tm['sibson_ms']:.3f} ms alone {ms:.3f} ms; rows/px mean "
           f"{rows.mean():.2f} p99 {np.percentile(rows, 99):.1f} max {rows.max():.1f}; nonfinite {int((~np.isfinite(d)).sum())}",
           flush=True)
