@@ -456,6 +456,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (const char* v = getenv("FOVRT_SHADE_XCD_BANDS")) c->xcd_bands = atoi(v) != 0;
   if (const char* v = getenv("FOVRT_SHADE_HANDOFF")) c->handoff = (uint32_t)std::min(std::max(atoi(v), 0), 2);
   if (const char* v = getenv("FOVRT_TEX_PACKING")) c->tex_packing = atoi(v) != 0;  // A/B knob: 0 = RGBA32F textures
+  if (const char* v = getenv("FOVRT_JFA_LAZY_OUTPUTS")) c->lazy_jfa_outputs = atoi(v) != 0;  // A/B knob
   if (const char* v = getenv("FOVRT_SIB_STRIP")) c->sib_strip = atoi(v) != 0;      // A/B knob: 0 = k_sibson_wide for the big discs
   {  // FOVRT_SLOTS: frame slots of the pipelined loop (2 or 3; A/B knob)
     const char* v = getenv("FOVRT_SLOTS");
@@ -874,7 +875,26 @@ static int enqueue_shading(fr_ctx* c) {
   return rc;
 }
 
+// JFA_COORD owed by the last JumpFlooding (launch_jfa with outputs = false), written on `s`, which the caller has
+// ordered after that JumpFlooding (from its final state and JFA_COLOR: nothing but the next JumpFlooding or a write of
+// JFA_COLOR changes those).
+static void materialize_jfa(fr_ctx* c, hipStream_t s) {
+  if (!c->jfa_coord_owed) return;
+  launch_jfa_coord(c->jfa_final, c->img[P_JFA_COLOR], c->img[P_JFA_COORD], c->W, c->H, s);
+  c->jfa_coord_owed = false;
+}
+static void join_recon(fr_ctx* c);
+// the same from an ABI call (on the context stream, after the pending reconstruction)
+static void materialize_jfa_now(fr_ctx* c) {
+  if (!c->jfa_coord_owed) return;
+  join_recon(c);
+  materialize_jfa(c, c->stream);
+}
+
 static int resolve(fr_ctx* c, int id, int* phys) {
+  // JFA_COORD read by a caller or a pass outside the frame chain, or JFA_COLOR about to be written: JFA_COORD is
+  // written first when owed
+  if (id == FR_BUF_JFA_COORD || id == FR_BUF_JFA_COLOR) materialize_jfa_now(c);
   switch (id) {
     case FR_BUF_POSITION: *phys = P_pos(c); return FR_OK;
     case FR_BUF_NORMAL: *phys = P_nrm(c); return FR_OK;
@@ -897,23 +917,30 @@ static int resolve(fr_ctx* c, int id, int* phys) {
   }
 }
 
+// JFA_COORD is written only when something asks for it (materialize_jfa: a caller's read, copy or view of a JFA
+// output, a pass reading one, a write of JFA_COLOR). Sibson's run form takes the seeds from the final state and a frame
+// reads nothing else of it: 133 MB less per 4K frame. (FOVRT_JFA_LAZY_OUTPUTS=0: always written.)
 static int enqueue_jfa(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {
   int p;
   if (resolve(c, in_buffer, &p)) return fail(c, FR_E_INVALID, "jfa: bad input buffer");
   const bool run_form = c->cfg.sibson_mode == 0;
+  const bool lazy = run_form && c->lazy_jfa_outputs;
   c->jfa_final = launch_jfa(c->img[p], c->jfa_a, c->jfa_b, c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->ftab, c->W,
-                            c->H, run_form ? c->sib_prefix : nullptr, run_form ? c->sib_blocks : nullptr,
+                            c->H, run_form ? c->sib_prefix : nullptr, run_form ? c->sib_blocks : nullptr, !lazy,
                             stream ? stream : c->stream);
+  c->jfa_coord_owed = lazy;
   c->sib_prefix_fresh = run_form;
   return check_launch(c);
 }
 static int enqueue_sibson(fr_ctx* c, hipStream_t stream = nullptr) {
-  if (c->cfg.sibson_mode == 1)  // per tap, bit-exact against the oracle
+  if (c->cfg.sibson_mode == 1) {  // per tap, bit-exact against the oracle (reads JFA_COORD)
+    materialize_jfa(c, stream ? stream : c->stream);
     launch_sibson(c->img[P_JFA_COORD], c->img[P_JFA_COLOR], c->img[P_SIBSON], c->W, c->H, stream ? stream : c->stream);
-  else  // run form (default): exact tap sets, rounding-level differences
+  } else {  // run form (default): exact tap sets, rounding-level differences
     launch_sibson_runs(c->img[P_JFA_COORD], c->jfa_final, c->img[P_JFA_COLOR], c->sib_prefix, c->sib_blocks, c->sib_rowp, c->sib_wide,
-                       c->sib_strips, c->img[P_SIBSON], c->W, c->H, c->sib_prefix_fresh, c->sib_strip,
+                       c->sib_strips, c->img[P_SIBSON], c->W, c->H, c->sib_prefix_fresh, c->sib_strip, c->jfa_coord_owed,
                        stream ? stream : c->stream);
+  }
   return check_launch(c);
 }
 static int enqueue_pullpush(fr_ctx* c, int in_buffer, hipStream_t stream = nullptr) {
@@ -1515,7 +1542,11 @@ int fr_gaze_target(fr_ctx* c, float xyz[3]) {
 }
 
 int fr_get_buffer(fr_ctx* c, int id, fr_buffer_view* v) {
+  const bool owed = c && c->jfa_coord_owed && (id == FR_BUF_JFA_COLOR || id == FR_BUF_JFA_COORD);
   const int rc = buffer_view(c, id, v);
+  // a view handed out after its image was written on demand: that write is complete when the call returns (the
+  // caller may read through the pointer on any stream)
+  if (rc == FR_OK && owed) HIP_TRY(c, hipStreamSynchronize(c->stream));
   // the caller may write the JFA outputs through the view: Sibson then derives its seeds and row prefix sums
   // from them again instead of from the JFA run's own state
   if (rc == FR_OK && (id == FR_BUF_JFA_COLOR || id == FR_BUF_JFA_COORD)) c->sib_prefix_fresh = false;

@@ -44,10 +44,11 @@ void launch_vring_pack(const f4*, int, int, int, const int32_t*, int, uint32_t*,
 void launch_vring_unpack(const uint32_t*, int, int, int, const int32_t*, int, f4*, hipStream_t);
 void launch_shard_unpack_active(const FrameUniforms&, const f4*, const uint32_t*, uint32_t, uint32_t, const f4*, const f4*, f4*,
                                 f4*, hipStream_t);
-const u2* launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, f4*, f4*, hipStream_t);
+const u2* launch_jfa(const f4*, u2*, u2*, f4*, f4*, const float*, int, int, f4*, f4*, bool, hipStream_t);
+void launch_jfa_coord(const u2*, const f4*, f4*, int, int, hipStream_t);
 void launch_sibson(const f4*, const f4*, f4*, int, int, hipStream_t);
 void launch_sibson_runs(const f4*, const u2*, const f4*, f4*, f4*, f4*, uint32_t*, uint32_t*, f4*, int, int, bool, bool,
-                        hipStream_t);
+                        bool, hipStream_t);
 int sibson_prefix_blocks(int W);
 size_t sibson_strip_words(int W, int H);
 size_t sibson_rowp_texels(int W, int H);
@@ -217,6 +218,10 @@ struct fr_ctx {
   bool sib_prefix_fresh = false;  // the last JFA wrote them with JFA_COLOR (cleared when JFA_COLOR / JFA_COORD are
                                   // written or handed out, fr_get_buffer)
   const u2* jfa_final = nullptr;  // that JFA's final state (the seeds k_sibson_runs reads while the prefix is fresh)
+  // JumpFlooding leaves JFA_COORD unwritten (the run form reads the seeds from jfa_final): while jfa_coord_owed,
+  // materialize_jfa writes it (k_jfa_coord, from jfa_final and JFA_COLOR) before anything reads it or writes JFA_COLOR.
+  bool jfa_coord_owed = false;
+  bool lazy_jfa_outputs = true;  // FOVRT_JFA_LAZY_OUTPUTS=0: every JumpFlooding writes JFA_COORD
   int pp_S = 0;
   DevStats* stats = nullptr;
   FrameUniforms U;

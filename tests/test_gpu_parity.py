@@ -1308,3 +1308,44 @@ def test_snapshot_restore_reproduces_next_frame(fovrt_mod):
         c.restore(snap)
     for t in (a, b, c):
         t.destroy()
+
+
+@pytest.mark.parametrize("W,H,gaze_deg", [(320, 192, None), (640, 360, 180.0)])
+def test_jfa_outputs_written_on_demand(fovrt_mod, monkeypatch, W, H, gaze_deg):
+    """JumpFlooding leaves JFA_COORD unwritten: Sibson's run form reads the seeds from the final JFA state, and
+    the context writes the image (from that state and JFA_COLOR) when something asks for it. Against contexts that
+    write it every time (FOVRT_JFA_LAZY_OUTPUTS=0), bit for bit: the outputs after pipelined frames (Sibson's wide and
+    big discs included: an off-centre gaze at 640x360), after the caller overwrote the JFA's input, and after
+    trace-only frames."""
+    monkeypatch.setenv("FOVRT_JFA_LAZY_OUTPUTS", "0")
+    eager = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    monkeypatch.delenv("FOVRT_JFA_LAZY_OUTPUTS")
+    lazy = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    cam = fovrt_mod.Camera.preset(1, W, H)
+    outs = (TN.JFA_COORD, TN.JFA_COLOR, TN.SIBSON, TN.PULLPUSH, TN.ATROUS, TN.SHADING)
+    for f in range(4):
+        cam.setPrevState()
+        cam.lookAt(np.asarray(cam.target) + np.array([0.01, 0.005, 0.0], np.float32))
+        for t in (eager, lazy):
+            t.update_optix_variables(cam)
+            if gaze_deg is not None:
+                a = np.deg2rad(gaze_deg)
+                t.set_gaze(W / 2 + 0.25 * H * np.cos(a), (H / 2 + 0.25 * H * np.sin(a)) / 1.25)
+            t.frame(timing=False)
+    for tid in outs:
+        assert equal_nan(lazy.read(tid), eager.read(tid)), ("after frames", tid)
+    # the JFA input overwritten by the caller before the owed outputs were read
+    for t in (eager, lazy):
+        t.frame(timing=False)
+        t.write(TN.SHADING, np.zeros((H, W, 4), np.float32))
+    for tid in (TN.JFA_COORD, TN.JFA_COLOR):
+        assert equal_nan(lazy.read(tid), eager.read(tid)), ("after a SHADING write", tid)
+    # trace-only frames: the slot holding the JFA's input comes round again
+    for t in (eager, lazy):
+        t.frame(timing=False)
+        for _ in range(4):
+            t.trace_frame(timing=False)
+    for tid in (TN.JFA_COORD, TN.JFA_COLOR):
+        assert equal_nan(lazy.read(tid), eager.read(tid)), ("after trace-only frames", tid)
+    eager.destroy()
+    lazy.destroy()
