@@ -165,11 +165,26 @@ def broadcast_id(dist, rank, make_id):
     return bytes(t.numpy().tobytes())
 
 
+def profile_paths(suffix):
+    """profiles/*_<suffix> newest first: the tag named in profiles/CURRENT (the last evidence run of the shipped
+    build, scripts/r06_evidence.sh) leads, then the rest by name."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_" + suffix)), reverse=True)
+    try:
+        with open(os.path.join(ROOT, "profiles", "CURRENT")) as f:
+            cur = os.path.join(ROOT, "profiles", f.read().strip() + "_" + suffix)
+    except OSError:
+        cur = None
+    if cur in paths:
+        paths.remove(cur)
+        paths.insert(0, cur)
+    return paths
+
+
 def load_traffic(kernels, config):
     """HBM bytes per launch of `kernels` from the newest profiles/*_pmc_traffic.json recorded on the
     same workload (scripts/profile.sh), else None."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+    for path in profile_paths("pmc_traffic.json"):
         try:
             with open(path) as f:
                 doc = json.load(f)
@@ -192,8 +207,7 @@ def load_traffic(kernels, config):
 def load_issue(kernel, config):
     """The SIMD issue picture of `kernel` from the newest profiles/*_pmc_issue.json recorded on the same
     workload (scripts/pmc_sq.sh + scripts/pmc_issue.py), else None."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_issue.json")), reverse=True):
+    for path in profile_paths("pmc_issue.json"):
         try:
             with open(path) as f:
                 doc = json.load(f)
