@@ -76,6 +76,8 @@ def test_gbuffer_bit_exact(fovrt_mod, oracle, scene, W, H):
 # set_gaze: on the top edge (gaze.y = H) and off the window (k_sampling clamps its focal-depth read).
 SAMPLING_CASES = ([(scene, m, 128, 96, None) for scene in (1, 2) for m in (0, 1, 2, 3, 4)]
                   + [(1, m, 100, 70, None) for m in (0, 4)]
+                  # W % 16 == 0 with a partial last block row: k_sampling's 16-byte mask rows, the rows below H skipped
+                  + [(1, m, 160, 72, None) for m in (0, 4)]
                   + [(2, 0, 100, 70, (50.0, 0.0)), (2, 0, 128, 96, (-30.0, 500.0)), (1, 4, 100, 70, (99.5, 0.0)),
                      (1, 0, 128, 96, (1e6, -1e6))]
                   # fractional cursors (glfw reports doubles, FR/gui.cpp:48-66): inexact gaze_dist products,
