@@ -457,6 +457,7 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
   if (const char* v = getenv("FOVRT_SHADE_HANDOFF")) c->handoff = (uint32_t)std::min(std::max(atoi(v), 0), 2);
   if (const char* v = getenv("FOVRT_TEX_PACKING")) c->tex_packing = atoi(v) != 0;  // A/B knob: 0 = RGBA32F textures
   if (const char* v = getenv("FOVRT_JFA_LAZY_OUTPUTS")) c->lazy_jfa_outputs = atoi(v) != 0;  // A/B knob
+  if (const char* v = getenv("FOVRT_EARLY_SETUP")) c->early_setup = atoi(v) != 0;            // A/B knob
   if (const char* v = getenv("FOVRT_SIB_STRIP")) c->sib_strip = atoi(v) != 0;      // A/B knob: 0 = k_sibson_wide for the big discs
   {  // FOVRT_SLOTS: frame slots of the pipelined loop (2 or 3; A/B knob)
     const char* v = getenv("FOVRT_SLOTS");
@@ -610,7 +611,9 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
       dalloc(&c->snap, pp_snap_count(c->pp_S)) != hipSuccess || dalloc(&c->stats, 1) != hipSuccess ||
       dalloc(&c->shade_ctr, shade_counter_words()) != hipSuccess || dalloc(&c->samples, std::max(N * cfg.spp, 2 * shade_fx_slots((uint32_t)N, cfg.spp, c->handoff))) != hipSuccess ||
       dalloc(&c->sample_help, std::max<size_t>(4 * shade_fx_slots((uint32_t)N, cfg.spp, c->handoff), 1)) != hipSuccess ||
-      dalloc(&c->aux, N) != hipSuccess || dalloc(&c->aux_seed, N) != hipSuccess ||
+      dalloc(&c->aux_p[0], N) != hipSuccess || dalloc(&c->aux_seed_p[0], N) != hipSuccess ||
+      dalloc(&c->aux_p[1], N) != hipSuccess || dalloc(&c->aux_seed_p[1], N) != hipSuccess ||
+      dalloc(&c->hvalid, N / 64 + 1) != hipSuccess ||
       hipMalloc((void**)&c->item_store, shade_item_store_f4() * sizeof(f4)) != hipSuccess ||
       (cfg.sibson_mode == 0 && (dalloc(&c->sib_prefix, (size_t)(c->W + 1) * c->H) != hipSuccess ||
                                 dalloc(&c->sib_blocks, (size_t)sibson_prefix_blocks(c->W) * c->H) != hipSuccess ||
@@ -620,6 +623,8 @@ int fr_create(const fr_config* cfg_in, fr_ctx** out) {
     c->err = "device allocation (work buffers) failed";
     return bail(FR_E_NOMEM);
   }
+  c->aux = c->aux_p[0];
+  c->aux_seed = c->aux_seed_p[0];
   {  // texel centres in texture coordinates, IEEE-correctly-rounded division as in the kernels
     std::vector<float> ft((size_t)c->W + c->H);
     for (int x = 0; x < c->W; x++) ft[x] = ((float)x + 0.5f) / (float)c->W;
@@ -676,7 +681,7 @@ int fr_destroy(fr_ctx* c) {
   fr(c->bcount); fr(c->shard_map); fr(c->front_need); fr(c->shade_radiance);
   if (c->h_counts) hipHostFree(c->h_counts);
   for (auto e : c->ev_counts) if (e) hipEventDestroy(e);
-  fr(c->gclass); fr(c->lp_cache); fr(c->lp_inv); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux); fr(c->aux_seed); fr(c->item_store); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
+  fr(c->gclass); fr(c->lp_cache); fr(c->lp_inv); fr(c->words); fr(c->counts); fr(c->offsets); fr(c->tiles); fr(c->shade_ctr); fr(c->samples); fr(c->sample_help); fr(c->aux_p[0]); fr(c->aux_p[1]); fr(c->aux_seed_p[0]); fr(c->aux_seed_p[1]); fr(c->hvalid); fr(c->item_store); fr(c->jfa_a); fr(c->jfa_b); fr(c->ftab);
   fr(c->pull); fr(c->push); fr(c->snap); fr(c->stats); fr(c->sib_prefix); fr(c->sib_blocks); fr(c->sib_wide); fr(c->sib_strips); fr(c->sib_rowp);
   for (auto e : c->ev) if (e) hipEventDestroy(e);
   if (c->ev_front) hipEventDestroy(c->ev_front);
@@ -754,6 +759,7 @@ static void join_recon(fr_ctx* c) {
 static int enqueue_geometry(fr_ctx* c, hipStream_t fs) {
   // a new frame: move to the next slot, once the reconstruction that read it has finished
   c->slot = (c->slot + 1) % c->nslots;
+  c->setup_early = false;
   const int sl = c->slot;
   c->mask = c->mask_p[sl]; c->active = c->active_p[sl]; c->ray_count = c->ray_count_p[sl];
   if (c->recon_pending[sl]) {
@@ -843,16 +849,27 @@ static int enqueue_shading(fr_ctx* c) {
     c->kt_pending++;
     hipEventRecord(kt[0], c->stream);
   }
+  // this frame's sample setup: enqueued by its front stages into the other aux buffer (frame_half), or here
+  if (c->setup_early) {
+    c->aux_i ^= 1;
+    c->aux = c->aux_p[c->aux_i];
+    c->aux_seed = c->aux_seed_p[c->aux_i];
+  }
+  const bool early = c->setup_early;
+  c->setup_early = false;
   // The inactive pixels' history carry (HBM-bound) touches no buffer k_shade_paths reads or writes:
-  // it runs on stream4 beside the latency-bound megakernel and joins before the resolve.
+  // it runs on stream4 beside the latency-bound megakernel and joins before the resolve. In latency mode, with one
+  // untiled view, it also writes the validity bits of the history this frame leaves (the next frame's early setup).
+  const bool hv = c->pipeline_mode == FR_PIPELINE_LATENCY && c->early_setup && c->U.shard_count <= 1 && !c->U.front_need;
   hipEventRecord(c->ev[11], c->stream);
   hipStreamWaitEvent(c->stream4, c->ev[11], 0);
   launch_carry_history(c->U, c->mask, c->img[P_wgt(c)], c->img[c->hist_cache], c->img[c->hist_cur],
-                       c->img[P_shd(c)], c->stream4);
+                       c->img[P_shd(c)], hv ? c->hvalid : nullptr, c->stream4);
   hipEventRecord(c->ev[12], c->stream4);
   const uint32_t N = (uint32_t)((size_t)c->W * c->H);
-  launch_sample_setup(c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache], c->aux, c->aux_seed,
-                      c->stream);
+  if (!early)
+    launch_sample_setup(c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache], nullptr, c->aux,
+                        c->aux_seed, c->stream);
   if (c->time_kernels) hipEventRecord(c->ev[9], c->stream);
   if (kt) hipEventRecord(kt[1], c->stream);
   launch_shade_paths(c->dsc, c->U, c->active, c->ray_count, N, c->img[P_wgt(c)], c->img[c->hist_cache],
@@ -871,6 +888,7 @@ static int enqueue_shading(fr_ctx* c) {
   int rc = check_launch(c);
   // swapBuffer("history_cache", "history_buffer"); swapBuffer("depth_cache", "depth_buffer") (:226-227)
   std::swap(c->hist_cur, c->hist_cache);
+  c->hvalid_fresh = hv;
   std::swap(c->depth_cur, c->depth_cache);
   return rc;
 }
@@ -1151,6 +1169,20 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
     if (t) hipEventRecord(ev[2], c->stream);
     if ((rc = enqueue_optimize(c, fs))) return rc;
     if (t) hipEventRecord(ev[3], c->stream);
+    if (latency && fs != c->stream && c->hvalid_fresh && c->U.shard_count <= 1 && !c->U.front_need && c->early_setup) {
+      // Early sample setup (latency mode): from the validity bits of the previous frame's history (its carry, ev[12])
+      // instead of the history itself, so it runs here with the front stages, and this frame's megakernel starts as
+      // soon as the previous frame's reconstruction ends (the setup sat between them on the context stream, ~0.1 ms
+      // on the CUs the reconstruction had just filled). Into the aux buffer the previous megakernel does not read.
+      // (Throughput mode keeps the setup after the resolve: there the megakernel then started beside the previous
+      // frame's reconstruction burst and ran 3.9 -> 4.1 ms, 240 -> 232 fps; profiles/r06_early_setup_ab.txt.)
+      hipStreamWaitEvent(fs, c->ev[12], 0);
+      const int o = c->aux_i ^ 1;
+      launch_sample_setup(c->U, c->active, c->ray_count, (uint32_t)((size_t)c->W * c->H), c->img[P_wgt(c)], nullptr,
+                          c->hvalid, c->aux_p[o], c->aux_seed_p[o], fs);
+      if ((rc = check_launch(c))) return rc;
+      c->setup_early = true;
+    }
     if (!t) {
       hipEventRecord(c->ev_front, fs);
       c->front_pending = true;
@@ -1272,6 +1304,7 @@ int fr_shard_unpack_active_enqueue(fr_ctx* c, const void* slab, size_t slab_byte
   const uint32_t* idx = (const uint32_t*)((const char*)slab + (size_t)capacity * sizeof(f4));
   launch_shard_unpack_active(c->U, vals, idx, count, (uint32_t)((size_t)c->W * c->H), c->img[P_wgt(c)],
                              c->img[c->hist_cur], c->img[c->hist_cache], c->img[P_shd(c)], c->stream);
+  c->hvalid_fresh = false;
   // the unpack reads the slot's WEIGHT: the front stages of frame + nslots (stream5 waits for ev_trace[slot])
   // may overwrite it only after this launch
   hipEventRecord(c->ev_trace[c->slot], c->stream);
@@ -1507,6 +1540,7 @@ int fr_shard_unpack_active(fr_ctx* c, const void* slab, size_t slab_bytes, uint3
   const uint32_t* idx = (const uint32_t*)((const char*)slab + (size_t)capacity * sizeof(f4));
   launch_shard_unpack_active(c->U, vals, idx, count, (uint32_t)((size_t)c->W * c->H), c->img[P_wgt(c)],
                              c->img[c->hist_cur], c->img[c->hist_cache], c->img[P_shd(c)], c->stream);
+  c->hvalid_fresh = false;
   int rc = check_launch(c);
   if (rc) return rc;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1550,6 +1584,8 @@ int fr_get_buffer(fr_ctx* c, int id, fr_buffer_view* v) {
   // the caller may write the JFA outputs through the view: Sibson then derives its seeds and row prefix sums
   // from them again instead of from the JFA run's own state
   if (rc == FR_OK && (id == FR_BUF_JFA_COLOR || id == FR_BUF_JFA_COORD)) c->sib_prefix_fresh = false;
+  // ... and the history: the next frame's sample setup then reads it, not the validity bits of what the last frame left
+  if (rc == FR_OK && (id == FR_BUF_HISTORY || id == FR_BUF_HISTORY_CACHE)) c->hvalid_fresh = false;
   return rc;
 }
 
@@ -1594,6 +1630,7 @@ int fr_write_buffer(fr_ctx* c, int id, const void* host, size_t bytes) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   // Sibson's row prefix sums (and the JFA state it reads its seeds from) no longer match these
   if (id == FR_BUF_JFA_COLOR || id == FR_BUF_JFA_COORD) c->sib_prefix_fresh = false;
+  if (id == FR_BUF_HISTORY || id == FR_BUF_HISTORY_CACHE) c->hvalid_fresh = false;
   if (id == FR_BUF_MASK) {
     // a host-written mask must also drive the compaction: rebuild the wave ballots from it
     c->compacted = false;
@@ -1713,6 +1750,7 @@ int fr_restore(fr_ctx* c, const void* host, size_t bytes) {
   c->lp_gaze = f2{-1e30f, -1e30f};  // the log-polar mask cache is recomputed for the restored gaze
   c->lp_mode = -1;
   c->sib_prefix_fresh = false;
+  c->hvalid_fresh = false;
   return FR_OK;
 }
 

@@ -18,13 +18,14 @@ void launch_shade_paths(const DevScene&, const FrameUniforms&, const uint32_t*, 
                         const f4*, uint32_t*, f4*, unsigned long long*, DevStats*, f4*, uint32_t*, uint32_t, uint32_t,
                         uint32_t, f4*, hipStream_t);
 size_t shade_item_store_f4();
-void launch_sample_setup(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*, f4*,
-                         uint32_t*, hipStream_t);
+void launch_sample_setup(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
+                         const unsigned long long*, f4*, uint32_t*, hipStream_t);
 void launch_shade_resolve(const FrameUniforms&, const uint32_t*, const uint32_t*, uint32_t, const f4*, const f4*,
                           const f4*, unsigned long long*, f4*, f4*, uint32_t*, uint32_t, f4*, hipStream_t);
 size_t shade_counter_words();
 size_t shade_fx_slots(uint32_t max_active, int spp, uint32_t handoff);
-void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, hipStream_t);
+void launch_carry_history(const FrameUniforms&, const uint8_t*, const f4*, const f4*, f4*, f4*, unsigned long long*,
+                          hipStream_t);
 void launch_sampling(const FrameUniforms&, const DevScene&, const f4*, const f4*, const f4*, f4*, const f4*,
                      const f4*, f4*, uint8_t*, const uint8_t*, unsigned long long*, uint32_t*, int, uint8_t*, uint32_t*,
                      bool, uint32_t*, hipStream_t);
@@ -203,8 +204,19 @@ struct fr_ctx {
   f4* samples = nullptr;          // one radiance value per (active pixel, camera sample): 16 B, or 32 B fixed point
   unsigned long long* sample_help = nullptr;  // fixed-point shares of the lanes that took over items, 32 B per sample
   f4* item_store = nullptr;     // the megakernel's refraction item stacks (shade_item_store_f4)
-  f4* aux = nullptr;              // per active pixel: NDC position, r1, r2 (k_sample_setup)
-  uint32_t* aux_seed = nullptr;   // per active pixel: the seed after the two draws
+  f4* aux = nullptr;              // per active pixel: NDC position, r1, r2 (k_sample_setup): aux_p[aux_i]
+  uint32_t* aux_seed = nullptr;   // per active pixel: the seed after the two draws: aux_seed_p[aux_i]
+  // Early sample setup (frame_half): a pipelined frame's k_sample_setup runs on the front stream right after its
+  // compaction, beside the previous frame's megakernel, into the other of two aux buffers, from the history validity
+  // bits (hvalid, one per pixel) the previous frame's k_carry_history computed. hvalid_fresh: those bits describe
+  // HISTORY_CACHE as the next frame will read it (cleared by anything else that writes the history).
+  f4* aux_p[2] = {};
+  uint32_t* aux_seed_p[2] = {};
+  int aux_i = 0;
+  unsigned long long* hvalid = nullptr;
+  bool hvalid_fresh = false;
+  bool setup_early = false;  // this frame's setup was enqueued by its front stages
+  bool early_setup = true;   // FOVRT_EARLY_SETUP=0: every setup on the context stream before its megakernel
   u2 *jfa_a = nullptr, *jfa_b = nullptr;  // JFA state ping-pong (seed coord texel + alpha flags)
   uint32_t chunk_refr = 0;  // fixed refraction-class chunk of the megakernel (FOVRT_SHADE_CHUNK_REFR), 0 adaptive
   uint32_t xcd_bands = 1;   // megakernel queue: per-XCD class bands (FOVRT_SHADE_XCD_BANDS=0: interleaved chunks)

@@ -323,6 +323,7 @@ int exchange(fr_group* g) {
       if (s != L.vrank && vring_sender(g, s))
         fr::launch_vring_unpack(L.vrecv[k][s], g->W, g->H, g->cfg.tile, L.tiles_dev + g->tile_off[s],
                                 g->tiles_per_vrank[s], L.c->img[L.c->hist_cache], L.c->stream);
+    L.c->hvalid_fresh = false;  // (the history no longer matches the validity bits of this frame's carry)
     if (int rc = fri::check_launch(L.c)) return gfail(rc, fr_last_error(L.c));
     hipEventRecord(L.ev_unpacked[k], L.c->stream);
     L.unpacked_pending[k] = true;
@@ -342,6 +343,7 @@ int exchange(fr_group* g) {
       fr::launch_shard_unpack_active(L.c->U, vals, idx, L.n[s], npix, L.c->img[fri::P_wgt(L.c)], L.c->img[L.c->hist_cur],
                                      L.c->img[L.c->hist_cache], L.c->img[fri::P_shd(L.c)], L.c->stream);
     }
+    L.c->hvalid_fresh = false;
     if (int rc = fri::check_launch(L.c)) return gfail(rc, fr_last_error(L.c));
     hipEventRecord(L.ev_unpacked[k], L.c->stream);
     L.unpacked_pending[k] = true;

@@ -723,6 +723,44 @@ def test_pipelined_frames_panning_equal_stage_calls(fovrt_mod, monkeypatch, slot
     assert a.ray_count() == b.ray_count()
 
 
+def test_early_sample_setup_equals_setup_after_resolve(fovrt_mod, monkeypatch):
+    """The early sample setup of latency mode (a frame's k_sample_setup on the front stream with its front stages,
+    from the history validity bits the previous frame's k_carry_history wrote) against the setup after the previous
+    resolve on the context stream (FOVRT_EARLY_SETUP=0): 12 frames, the camera panning and the gaze
+    moving every frame (the seeds' validity comes from reprojected pixels), a light change (the accumulation
+    restarts at frame 0, which clears the history), a timed frame, and a host write of HISTORY_CACHE that leaves
+    part of the history invalid (the next frame must not use the bits of the history before the write). Bit for
+    bit, frame by frame at the checkpoints."""
+    W, H = 320, 192
+    a = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    monkeypatch.setenv("FOVRT_EARLY_SETUP", "0")
+    b = make_tracer(fovrt_mod, W, H, scene=1, mask=4, spp=4, dmd=3)
+    monkeypatch.delenv("FOVRT_EARLY_SETUP")
+    for t in (a, b):
+        t.set_pipeline_mode(fovrt_mod.PIPELINE_LATENCY)
+    cam = fovrt_mod.Camera.preset(1, W, H)
+    hist = np.zeros((H, W, 4), np.float32)
+    hist[:, : W // 2] = (0.25, 0.5, 0.75, 1.0)  # the right half's history invalid (.w = 0)
+    outs = (TN.SHADING, TN.HISTORY_CACHE, TN.SIBSON, TN.ATROUS, TN.MASK, TN.WEIGHT)
+    for f in range(12):
+        cam.setPrevState()
+        cam.lookAt(np.asarray(cam.target) + np.array([0.01, 0.005, 0.0], np.float32))
+        for t in (a, b):
+            t.update_optix_variables(cam)
+            t.set_gaze(W / 2 + 30 * np.cos(f), (H / 2 + 30 * np.sin(f)) / 1.25)
+            if f == 4:
+                t.set_light_power(0.8)
+            if f == 7:
+                t.write(TN.HISTORY_CACHE, hist)
+            t.frame(timing=f == 9)
+        if f in (3, 8, 11):
+            for tid in outs:
+                assert equal_nan(a.read(tid), b.read(tid)), (f, tid)
+    assert a.ray_count() == b.ray_count()
+    for t in (a, b):
+        t.destroy()
+
+
 def test_latency_pipeline_mode_equals_throughput_mode(fovrt_mod):
     """fr_set_pipeline_mode(FR_PIPELINE_LATENCY) (one trace half in flight; the host waits for the previous
     frame's path trace) renders the same frames as the default throughput pipelining, bit for bit, with
