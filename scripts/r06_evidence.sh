@@ -17,6 +17,7 @@ bash scripts/profile.sh "$TAG" --steps 20 --warmup 5 > gpurun_out/${TAG}_profile
 head -12 gpurun_out/${TAG}_profile.txt; keep
 bash scripts/pmc_sq.sh || exit 3
 python3 scripts/pmc_issue.py gpurun_out "$TAG" > gpurun_out/${TAG}_issue.txt 2>&1 || exit 3
+echo "$TAG" > profiles/CURRENT  # the bench below quotes this run's traffic and issue profiles
 keep
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit 4
 python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_bench.json'));r=d['roofline'];print('bench', d['value'], d['fps'], d['fps_serial_mean'], d['pipeline_latency_mode']['fps'], r['megakernel_ms'], r['megakernel_ms_serialised'], r.get('traffic'), d['cpu_baseline'].get('value'))"
