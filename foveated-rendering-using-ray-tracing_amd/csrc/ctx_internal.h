@@ -206,10 +206,10 @@ struct fr_ctx {
   f4* item_store = nullptr;     // the megakernel's refraction item stacks (shade_item_store_f4)
   f4* aux = nullptr;              // per active pixel: NDC position, r1, r2 (k_sample_setup): aux_p[aux_i]
   uint32_t* aux_seed = nullptr;   // per active pixel: the seed after the two draws: aux_seed_p[aux_i]
-  // Early sample setup (frame_half): a pipelined frame's k_sample_setup runs on the front stream right after its
-  // compaction, beside the previous frame's megakernel, into the other of two aux buffers, from the history validity
-  // bits (hvalid, one per pixel) the previous frame's k_carry_history computed. hvalid_fresh: those bits describe
-  // HISTORY_CACHE as the next frame will read it (cleared by anything else that writes the history).
+  // Early sample setup (frame_half, latency mode): a frame's k_sample_setup runs on the front stream right after its
+  // compaction, into the other of two aux buffers, from the history validity bits (hvalid, one per pixel) the previous
+  // frame's k_carry_history computed. hvalid_fresh: those bits describe HISTORY_CACHE as the next frame will read it
+  // (cleared by anything else that writes the history).
   f4* aux_p[2] = {};
   uint32_t* aux_seed_p[2] = {};
   int aux_i = 0;
