@@ -1140,8 +1140,13 @@ static int frame_half(fr_ctx* c, fr_frame_timing* t, bool trace, bool recon) {
       // Only half of the front stages' span is overlapped: the big discs' strip kernel fills every CU, and a
       // front stage started further into it ran ~4 ms instead of ~1, with its gaze sampled that much earlier
       // (eye-tracked circle latency p99 16.2 -> 12.6 ms at 142 fps; C3 p50 6.15 -> 5.81 ms; overlapping none:
-      // p99 12.5 ms at 139 fps, the serial loop's rate). FOVRT_LAT_OVERLAP: the percentage (A/B knob).
-      static const float ovl = [] { const char* v = getenv("FOVRT_LAT_OVERLAP"); return v ? atoi(v) / 100.0f : 0.5f; }();
+      // p99 12.5 ms at 139 fps, the serial loop's rate). A short Sibson (no big discs: below kLatShortSibMs) takes the
+      // whole span: the front stages then end with it without slowing down (4K bunny centred 186.0 -> 189.3 fps at
+      // latency p50 5.72 -> 5.79 ms, 4K vokselia 233.1 -> 235.2 fps; profiles/r06_lat_overlap_*). FOVRT_LAT_OVERLAP:
+      // one percentage for every frame instead (A/B knob).
+      constexpr float kLatShortSibMs = 1.5f;
+      static const float ovl_env = [] { const char* v = getenv("FOVRT_LAT_OVERLAP"); return v ? atoi(v) / 100.0f : -1.0f; }();
+      const float ovl = ovl_env >= 0.0f ? ovl_env : c->lat_sib_ms < kLatShortSibMs ? 1.0f : 0.5f;
       const float delay_ms = c->jfa_pending[prev] ? c->lat_sib_ms - ovl * c->lat_front_ms : 0.0f;
       if (delay_ms > 0.05f) {
         const auto t0 = std::chrono::steady_clock::now();
